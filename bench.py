@@ -1,0 +1,165 @@
+#!/usr/bin/env python3
+"""Benchmark: batched KKT Newton-steps/sec of the parallel-in-time IPM hot path on MI355X.
+
+Metric (BASELINE.json): "KKT Newton-steps/sec at (horizon N x batch)".  One step = one batched
+KKT solve (paroc.par_bwd_pass + par_fwd_pass replacement, noc_kkt_solve) of `batch` cart-pole
+trajectories with horizon N = 200 (BASELINE config c3), the LQ blocks being the real first
+Newton iterate (bp = 0.1) produced on the device by the linearisation kernels, resident in HBM
+before timing.  value = trajectories x steps / second, summed over ranks (weak scaling: every
+rank owns `batch` trajectories; no collective on the data path, one all-reduce(max) of the
+timing).  Roofline: algorithmic bytes per launch / measured launch time vs the
+8 TB/s HBM peak.  cpu_baseline: the plain-C restatement of the reference's sequential Riccati
+(oracle/kkt_ref.c, OpenMP) on a bounded sample of the same blocks, rank 0, N=1 only.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ip-parallel-optimal-control_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def algorithmic_bytes(nx, nu, N, B):
+    """read A,B,Q,M,R,ru once + write dx,du once per stage, + P per trajectory."""
+    per_stage = 8 * (2 * nx * nx + 2 * nx * nu + nu * nu + nu + nx + nu)
+    return B * N * per_stage + B * 8 * nx * nx
+
+
+def pmc_traffic(path, kernel_substr):
+    """HBM bytes per launch of the KKT kernel from a committed rocprofv3 --pmc summary (JSON written
+    by tools/pmc_traffic.py), or None."""
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return d.get(kernel_substr)
+    except Exception:
+        return None
+
+
+def cpu_baseline(blocks, sample, seconds=10.0):
+    """Time the C restatement of the sequential KKT solve on `sample` trajectories."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    from oracle import kkt_ref
+    idx = list(range(sample))
+    host = {k: blocks[k][idx].cpu().numpy() for k in ("A", "B", "Q", "R", "M", "r", "P", "reg")}
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    kkt_ref.solve(*(host[k] for k in ("A", "B", "Q", "R", "M", "r", "P", "reg")), threads=cores)
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        kkt_ref.solve(*(host[k] for k in ("A", "B", "Q", "R", "M", "r", "P", "reg")), threads=cores)
+        reps += 1
+    dt = time.perf_counter() - t0
+    return dict(value=reps * sample / dt, unit="trajectory-KKT-steps/s", cores=cores, kind="port",
+                sample=f"{sample} cart-pole trajectories x N={host['A'].shape[1]}, {reps} repeats "
+                       f"({dt:.1f} s) of the OpenMP C sequential Riccati (oracle/kkt_ref.c)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--problem", default="cartpole")
+    ap.add_argument("--horizon", type=int, default=200)
+    ap.add_argument("--batch", type=int, default=4096, help="trajectories per GPU")
+    ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-sample", type=int, default=512)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from noc import lqt, problems, _lib
+
+    N, B = args.horizon, args.batch
+    blocks = problems.make_bench_blocks(args.problem, N=N, batch=B, seed=1234 + rank)
+    nx, nu = blocks["A"].shape[-1], blocks["B"].shape[-1]
+    lanes = args.lanes or _lib.load().noc_kkt_default_lanes(nx, nu, N)
+    out = lqt.kkt_solve(blocks["A"], blocks["B"], blocks["Q"], blocks["R"], blocks["M"],
+                        blocks["r"], blocks["P"], reg=blocks["reg"], lanes=lanes)
+
+    def step():
+        lqt.kkt_solve(blocks["A"], blocks["B"], blocks["Q"], blocks["R"], blocks["M"], blocks["r"],
+                      blocks["P"], reg=blocks["reg"], lanes=lanes, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kern_ms = ev0.elapsed_time(ev1) / args.steps          # HIP-event time per launch (stream)
+    ms = wall * 1e3 / args.steps
+    if world > 1:
+        t = torch.tensor([ms, kern_ms], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms, kern_ms = float(t[0]), float(t[1])
+    feasible_frac = float(out.feasible.float().mean())
+    value = world * B * args.steps / (ms * args.steps / 1e3)
+    abytes = algorithmic_bytes(nx, nu, N, B)
+    achieved = abytes / (kern_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(args.pmc_json, f"{args.problem}_N{N}_B{B}")
+    result = {
+        "metric": "KKT Newton-steps/sec at (horizon N x batch)",
+        "value": value,
+        "unit": "trajectory-KKT-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: first Newton iterate (bp=0.1) of random-start cart-pole problems, "
+                "linearised on device",
+        "config": {"workload": f"{args.problem} nx={nx} nu={nu} N={N} batch={B}/GPU "
+                               f"(BASELINE c3; c5 when run on 8 GPUs)",
+                   "horizon": N, "batch_per_gpu": B, "global_batch": B * world,
+                   "lanes_per_trajectory": lanes, "parallelism": f"trajectory-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes_per_launch": abytes, "kernel_ms": kern_ms},
+        "feasible_fraction": feasible_frac,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            result["cpu_baseline"] = cpu_baseline(blocks, min(args.cpu_sample, B), args.cpu_seconds)
+        except Exception as e:  # reported, never fatal
+            result["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

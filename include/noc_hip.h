@@ -1,0 +1,130 @@
+/* noc_hip.h -- C-ABI of libnoc_hip.so, the MI355X (gfx950) hot path of the interior-point
+ * trajectory optimiser.  Plain pointers and sizes only; all arrays are fp64 device pointers
+ * (hipMalloc / torch data_ptr), row-major, contiguous, 16-byte aligned; every call is
+ * asynchronous on `stream` (a hipStream_t, NULL = default stream) and never synchronises.
+ *
+ * Return value: 0 on success, < 0 on an argument or HIP error (noc_last_error() explains).
+ * Numerical trouble is data, never an error: feasible[b] = 0, pred NaN/inf, exactly like the
+ * reference's jnp.where / NaN semantics (noc/par_interior_point_newton.py:159-173).
+ *
+ * LQ sub-problem solved per trajectory b (shapes per trajectory; leading batch axis B):
+ *   stage k < N : 1/2 x'Q_k x + x'M_k u + 1/2 u'(R_k + reg_b I)u + r_k'u + q_k'x
+ *   dynamics    : x_{k+1} = A_k x_k + Bm_k u_k + c_k,   x_0 = x0
+ *   terminal    : 1/2 x_N'P x_N + p'x_N
+ *   A [B][N][nx][nx]  Bm [B][N][nx][nu]  Q [B][N][nx][nx]  R [B][N][nu][nu]  M [B][N][nx][nu]
+ *   r [B][N][nu]      q, c [B][N][nx] (NULL = 0)   P [B][nx][nx]   p, x0 [B][nx] (NULL = 0)
+ *   reg [B] (NULL = 0)                              active [B] int32 (NULL = all; 0 = skip)
+ * Outputs:
+ *   dx [B][N+1][nx]  du [B][N][nu]  pred [B]  feasible [B] int32
+ *   K [B][N][nu][nx] d [B][N][nu]   (du_k = K_k dx_k + d_k)   -- always written (workspace)
+ *   S [B][N+1][nx][nx]  v [B][N+1][nx]  (V_k(x) = 1/2 x'S_k x + v_k'x; NULL = not written)
+ *   pred = sum_k d_k'Qu_k + 1/2 d_k'Quu_k d_k,  feasible = all_k Quu_k > 0
+ *
+ * Supported (nx, nu): (2,1) pendulum, (4,1) cart-pole, (8,4) stacked double integrators.
+ * `lanes` = lanes of a wave64 per trajectory (64, 32, 16, 8); 0 = library default.
+ */
+#ifndef NOC_HIP_H
+#define NOC_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NOC_ABI_VERSION 1
+
+/* Library identity / diagnostics. */
+int noc_abi_version(void);
+const char* noc_last_error(void);
+int noc_kkt_supported(int nx, int nu);
+int noc_kkt_default_lanes(int nx, int nu, int N);
+
+/* Fused batched KKT solve of one Newton step: par_bwd_pass + par_fwd_pass.
+ * Replaces par_Newton's solver calls, noc/par_interior_point_newton.py:119-123
+ * (paroc.par_bwd_pass(lqt) -> Kx, d, S, v, pred, feasible; paroc.par_fwd_pass(lqt, 0, Kx, d)). */
+int noc_kkt_solve(int nx, int nu, int N, int B, int lanes,
+                  const double* A, const double* Bm, const double* Q, const double* R,
+                  const double* M, const double* r, const double* q, const double* c,
+                  const double* P, const double* p, const double* x0, const double* reg,
+                  const int* active,
+                  double* dx, double* du, double* pred, int* feasible,
+                  double* K, double* d, double* S, double* v, void* stream);
+
+/* Backward pass only: replaces paroc.par_bwd_pass (call sites
+ * noc/par_interior_point_newton.py:120, examples/linear_mpc_parallel.py:68). */
+int noc_par_bwd_pass(int nx, int nu, int N, int B, int lanes,
+                     const double* A, const double* Bm, const double* Q, const double* R,
+                     const double* M, const double* r, const double* q, const double* c,
+                     const double* P, const double* p, const double* reg, const int* active,
+                     double* K, double* d, double* S, double* v, double* pred, int* feasible,
+                     void* stream);
+
+/* Forward pass only: replaces paroc.par_fwd_pass(lqt, x0, Kx, d) -> (u, x) (call sites
+ * noc/par_interior_point_newton.py:121-123, examples/linear_mpc_parallel.py:69).
+ * K and d are inputs here. */
+int noc_par_fwd_pass(int nx, int nu, int N, int B, int lanes,
+                     const double* A, const double* Bm, const double* c, const double* x0,
+                     const double* K, const double* d, const int* active,
+                     double* du, double* dx, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Batched interior-point driver kernels for registered problem families.
+ * Replaces the device-side body of par_interior_point_optimal_control / newton_oc
+ * (noc/par_interior_point_newton.py:127-254) and, with mode NOC_MODE_SEQ, of
+ * seq_interior_point_optimal_control (noc/seq_interior_point_newton.py:108-202).
+ * The host loop calls noc_ipm_step until no trajectory's phase is NOC_PHASE_DONE-pending.
+ * ------------------------------------------------------------------------------------------ */
+#define NOC_FAMILY_PENDULUM 1 /* examples/pendulum_runtime.py:19-72 */
+#define NOC_FAMILY_CARTPOLE 2 /* examples/cartpole_runtime.py:18-82 */
+#define NOC_FAMILY_LINEAR 3   /* examples/linear_mpc_parallel.py:24-63, linear_demo_cuda.py */
+
+#define NOC_PHASE_ROLLOUT 0
+#define NOC_PHASE_LINEARIZE 1
+#define NOC_PHASE_SOLVE 2
+#define NOC_PHASE_DONE 3
+
+#define NOC_MODE_PAR 0 /* par_interior_point_newton semantics (retry loop, reg = rp*|cu|) */
+#define NOC_MODE_SEQ 1 /* seq_interior_point_newton semantics (one accept/reject, reg = mu) */
+
+#define NOC_TERMINAL_FINAL_COST 0 /* terminal Hessian = hessian(final_cost)(x_N)  (S:66) */
+#define NOC_TERMINAL_STAGE0 1     /* the reference par path's XT = Q[0]           (P:73) */
+
+/* Problem family descriptor.  Stage cost:
+ *   1/2 sum_i wx_i e_i^2 + 1/2 sum_j wu_j u_j^2 - bp sum_j [log(ub - u_j) + log(u_j + ub)]
+ * with e = x - goal (state wrap_index taken mod 2*pi first); the barrier term is absent when
+ * u_bound <= 0.  Terminal cost 1/2 sum_i wf_i e_i^2.  Dynamics: Euler(ode, dt) for the pendulum
+ * and cart-pole, x+ = A x + B u for LINEAR. */
+typedef struct noc_family {
+  int kind, nx, nu, wrap_index;
+  double dt, u_bound;
+  double goal[8], wx[8], wu[4], wf[8];
+  double A[64], B[32];
+} noc_family;
+
+/* Workspace of device pointers (all fp64 unless noted; Bt trajectories, horizon N). */
+typedef struct noc_ipm_ws {
+  int Bt, N;
+  double *x, *u, *x0;                  /* (Bt,N+1,nx) (Bt,N,nu) (Bt,nx)           */
+  double *A, *B, *Q, *R, *M, *r, *P;   /* LQ blocks, layouts as noc_kkt_solve      */
+  double *cx, *cu, *lc, *lam;          /* (Bt,N,nx) (Bt,N,nu) (Bt,N) (Bt,N+1,nx)    */
+  double *dx, *du, *pred, *K, *d;      /* KKT outputs                              */
+  int *feasible;                       /* (Bt) int32                               */
+  int *phase, *kkt_active, *it, *inner, *total_it, *kkt_solves; /* (Bt) int32     */
+  double *bp, *rp, *rinc, *cost, *hu, *gnorm, *reg;              /* (Bt)           */
+} noc_ipm_ws;
+
+int noc_family_supported(const noc_family* fam);
+/* state <- start of the barrier schedule (bp = bp0, rp = 1, r_inc = 2, phase ROLLOUT). */
+int noc_ipm_init(const noc_ipm_ws* ws, double bp0, void* stream);
+/* rollout (phase ROLLOUT) + linearise / costates / LQ blocks (phase LINEARIZE) -> phase SOLVE. */
+int noc_ipm_prepare(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal,
+                    void* stream);
+/* trial point, gain ratio, regularisation update, accept, stop test, barrier schedule. */
+int noc_ipm_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* stream);
+/* one device iteration: prepare + noc_kkt_solve(active = phase != DONE) + trial. */
+int noc_ipm_step(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, int lanes,
+                 void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NOC_HIP_H */

@@ -1,0 +1,444 @@
+// Interior-point Newton loop kernels for the registered problem families (fp64, gfx950).
+//
+// One host iteration of the batched driver (noc/par_interior_point_newton.py of this package)
+// launches, each masked by the per-trajectory phase so every trajectory follows its own
+// reference control flow (vmap semantics of the reference's nested while_loops):
+//   rollout   (phase ROLLOUT)   noc/utils.py:57-63, at the start of each barrier stage (P:133)
+//   linearize (phase LINEARIZE) derivatives of P:13-28 at (x_k, u_k): A=fx, B=fu, cx, cu, l_k
+//   costate   (phase LINEARIZE) lambda scan C:43-54 + ru = cu + fu' lambda (P:34), total cost
+//                               (P:142), |Hu|inf (P:158), ||cu||_F (P:116), terminal Hessian
+//   assemble  (phase LINEARIZE) Q, R, M of compute_lqr_params (P:31-42)
+//   [kkt_scan (phase SOLVE)     par_Newton's solve, P:119-123]
+//   trial     (phase SOLVE)     trial point, feasibility, gain ratio, rp / r_inc update, accept,
+//                               Newton stop test, barrier schedule (P:156-254; seq mode S:121-202)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "../../include/noc_hip.h"
+#include "families_gen.h"
+#include "noc_internal.h"
+#include "small_linalg.h"
+
+namespace noc {
+
+constexpr double kTwoPi = 6.283185307179586;  // 2.0 * jnp.pi
+
+// noc/utils.py:8-10 with jnp.remainder semantics (C fmod, + divisor if the sign differs)
+NOC_DEV double wrap_angle(double a) {
+  double r = fmod(a, kTwoPi);
+  return (r != 0.0 && r < 0.0) ? r + kTwoPi : r;
+}
+
+template <int KIND, int NX, int NU>
+struct Fam {
+  const noc_family& p;
+  NOC_DEV explicit Fam(const noc_family& prm) : p(prm) {}
+
+  // ------------------------------------------------------------------ dynamics
+  NOC_DEV void step(const double* x, const double* u, double* xn) const {
+    if constexpr (KIND == NOC_FAMILY_LINEAR) {
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        double t = 0.0;
+        NOC_UNROLL for (int k = 0; k < NX; ++k) t += p.A[i * NX + k] * x[k];
+        NOC_UNROLL for (int j = 0; j < NU; ++j) t += p.B[i * NU + j] * u[j];
+        xn[i] = t;
+      }
+    } else {
+      double f[NX];
+      if constexpr (KIND == NOC_FAMILY_PENDULUM) gen::pendulum_ode(x, u, f);
+      else gen::cartpole_ode(x, u, f);
+      NOC_UNROLL for (int i = 0; i < NX; ++i) xn[i] = x[i] + p.dt * f[i];  // noc/utils.py:50-54
+    }
+  }
+  NOC_DEV void jac(const double* x, const double* u, double* fx, double* fu) const {
+    if constexpr (KIND == NOC_FAMILY_LINEAR) {
+      NOC_UNROLL for (int i = 0; i < NX * NX; ++i) fx[i] = p.A[i];
+      NOC_UNROLL for (int i = 0; i < NX * NU; ++i) fu[i] = p.B[i];
+    } else {
+      constexpr int NZ = NX + NU;
+      double J[NX * NZ];
+      if constexpr (KIND == NOC_FAMILY_PENDULUM) gen::pendulum_ode_jac(x, u, J);
+      else gen::cartpole_ode_jac(x, u, J);
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        NOC_UNROLL for (int j = 0; j < NX; ++j) fx[i * NX + j] = (i == j ? 1.0 : 0.0) + p.dt * J[i * NZ + j];
+        NOC_UNROLL for (int j = 0; j < NU; ++j) fu[i * NU + j] = p.dt * J[i * NZ + NX + j];
+      }
+    }
+  }
+  // sum_i lam_i d2 f_i (Euler: dt * ode Hessians); adds into Hxx (NXxNX), Huu, Hxu (NXxNU)
+  NOC_DEV void add_hess_l(const double* x, const double* u, const double* lam, double* Hxx,
+                          double* Huu, double* Hxu) const {
+    if constexpr (KIND != NOC_FAMILY_LINEAR) {
+      constexpr int NZ = NX + NU;
+      double H[NZ * NZ];
+      if constexpr (KIND == NOC_FAMILY_PENDULUM) gen::pendulum_ode_hess_l(x, u, lam, H);
+      else gen::cartpole_ode_hess_l(x, u, lam, H);
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        NOC_UNROLL for (int j = 0; j < NX; ++j) Hxx[i * NX + j] += p.dt * H[i * NZ + j];
+        NOC_UNROLL for (int j = 0; j < NU; ++j) Hxu[i * NU + j] += p.dt * H[i * NZ + NX + j];
+      }
+      NOC_UNROLL for (int i = 0; i < NU; ++i)
+        NOC_UNROLL for (int j = 0; j < NU; ++j) Huu[i * NU + j] += p.dt * H[(NX + i) * NZ + NX + j];
+    }
+  }
+
+  // ------------------------------------------------------------------ costs
+  NOC_DEV double err(const double* x, int i) const {
+    const double xi = (i == p.wrap_index) ? wrap_angle(x[i]) : x[i];
+    return xi - p.goal[i];
+  }
+  NOC_DEV bool barrier() const { return p.u_bound > 0.0; }
+  // stage cost (PR:40-50 / CR:36-45 / LD:138-141)
+  NOC_DEV double stage_cost(const double* x, const double* u, double bp) const {
+    double c = 0.0;
+    NOC_UNROLL for (int i = 0; i < NX; ++i) { const double e = err(x, i); c += p.wx[i] * e * e; }
+    c *= 0.5;
+    double cu = 0.0;
+    NOC_UNROLL for (int j = 0; j < NU; ++j) cu += p.wu[j] * u[j] * u[j];
+    c += 0.5 * cu;
+    if (barrier()) {
+      double lb = 0.0;
+      NOC_UNROLL for (int j = 0; j < NU; ++j) lb += log(p.u_bound - u[j]) + log(u[j] + p.u_bound);
+      c -= bp * lb;
+    }
+    return c;
+  }
+  NOC_DEV void stage_grad(const double* x, const double* u, double bp, double* cx,
+                          double* cu) const {
+    NOC_UNROLL for (int i = 0; i < NX; ++i) cx[i] = p.wx[i] * err(x, i);
+    NOC_UNROLL for (int j = 0; j < NU; ++j) {
+      double g = p.wu[j] * u[j];
+      if (barrier()) g += bp / (p.u_bound - u[j]) - bp / (u[j] + p.u_bound);
+      cu[j] = g;
+    }
+  }
+  NOC_DEV double stage_cuu(const double* u, double bp, int j) const {
+    double h = p.wu[j];
+    if (barrier()) {
+      const double a = p.u_bound - u[j], b = u[j] + p.u_bound;
+      h += bp / (a * a) + bp / (b * b);
+    }
+    return h;
+  }
+  NOC_DEV bool feasible(const double* u) const {  // all(constraints <= 0) (P:45-47)
+    if (!barrier()) return true;
+    bool ok = true;
+    NOC_UNROLL for (int j = 0; j < NU; ++j) ok = ok && (u[j] - p.u_bound <= 0.0) && (-u[j] - p.u_bound <= 0.0);
+    return ok;
+  }
+  NOC_DEV double final_cost(const double* x) const {
+    double c = 0.0;
+    NOC_UNROLL for (int i = 0; i < NX; ++i) { const double e = err(x, i); c += p.wf[i] * e * e; }
+    return 0.5 * c;
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+template <int KIND, int NX, int NU>
+__global__ __launch_bounds__(256) void rollout_kernel(noc_family prm, noc_ipm_ws w) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= w.Bt || w.phase[b] != NOC_PHASE_ROLLOUT) return;
+  Fam<KIND, NX, NU> f(prm);
+  const int N = w.N;
+  double x[NX];
+  NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = w.x0[(size_t)b * NX + i];
+  double* X = w.x + (size_t)b * (N + 1) * NX;
+  const double* U = w.u + (size_t)b * N * NU;
+  NOC_UNROLL for (int i = 0; i < NX; ++i) X[i] = x[i];
+  for (int k = 0; k < N; ++k) {
+    double u[NU], xn[NX];
+    NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = U[(size_t)k * NU + j];
+    f.step(x, u, xn);
+    NOC_UNROLL for (int i = 0; i < NX; ++i) { x[i] = xn[i]; X[(size_t)(k + 1) * NX + i] = xn[i]; }
+  }
+  w.phase[b] = NOC_PHASE_LINEARIZE;
+}
+
+template <int KIND, int NX, int NU>
+__global__ __launch_bounds__(256) void linearize_kernel(noc_family prm, noc_ipm_ws w) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = w.N;
+  if (t >= (long long)w.Bt * N) return;
+  const int b = (int)(t / N), k = (int)(t % N);
+  if (w.phase[b] != NOC_PHASE_LINEARIZE) return;
+  Fam<KIND, NX, NU> f(prm);
+  const double bp = w.bp[b];
+  double x[NX], u[NU];
+  gload<NX>(w.x + ((size_t)b * (N + 1) + k) * NX, x);
+  NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = w.u[(size_t)t * NU + j];
+  double fx[NX * NX], fu[NX * NU], cx[NX], cu[NU];
+  f.jac(x, u, fx, fu);
+  f.stage_grad(x, u, bp, cx, cu);
+  gstore<NX * NX>(w.A + (size_t)t * NX * NX, fx);
+  gstore<NX * NU>(w.B + (size_t)t * NX * NU, fu);
+  gstore<NX>(w.cx + (size_t)t * NX, cx);
+  NOC_UNROLL for (int j = 0; j < NU; ++j) w.cu[(size_t)t * NU + j] = cu[j];
+  w.lc[t] = f.stage_cost(x, u, bp);
+}
+
+// one thread per trajectory: sequential costate recursion (C:43-54) + per-trajectory scalars
+template <int KIND, int NX, int NU>
+__global__ __launch_bounds__(256) void costate_kernel(noc_family prm, noc_ipm_ws w, int mode) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= w.Bt || w.phase[b] != NOC_PHASE_LINEARIZE) return;
+  Fam<KIND, NX, NU> f(prm);
+  const int N = w.N;
+  const size_t bN = (size_t)b * N;
+  const double* xN = w.x + ((size_t)b * (N + 1) + N) * NX;
+  double xf[NX], lam[NX];
+  NOC_UNROLL for (int i = 0; i < NX; ++i) xf[i] = xN[i];
+  // lambda_N = grad final_cost (C:44); terminal Hessian = hessian(final_cost) (S:66)
+  NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = prm.wf[i] * f.err(xf, i);
+  double* L = w.lam + (size_t)b * (N + 1) * NX;
+  NOC_UNROLL for (int i = 0; i < NX; ++i) L[(size_t)N * NX + i] = lam[i];
+  double P[NX * NX];
+  NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) P[i * NX + j] = (i == j) ? prm.wf[i] : 0.0;
+  gstore<NX * NX>(w.P + (size_t)b * NX * NX, P);
+  double cost = f.final_cost(xf);
+  double hu = 0.0, g2 = 0.0;
+  for (int k = N - 1; k >= 0; --k) {
+    const size_t t = bN + k;
+    double A[NX * NX], Bm[NX * NU], cx[NX];
+    gload<NX * NX>(w.A + t * NX * NX, A);
+    gload<NX * NU>(w.B + t * NX * NU, Bm);
+    gload<NX>(w.cx + t * NX, cx);
+    // ru_k = cu_k + fu_k' lambda_{k+1}  (P:34)
+    NOC_UNROLL for (int j = 0; j < NU; ++j) {
+      const double cu = w.cu[t * NU + j];
+      double r = cu;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) r += Bm[i * NU + j] * lam[i];
+      w.r[t * NU + j] = r;
+      hu = fmax(hu, fabs(r));
+      g2 += cu * cu;
+    }
+    double ln[NX];
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      double s = cx[i];
+      NOC_UNROLL for (int m = 0; m < NX; ++m) s += A[m * NX + i] * lam[m];
+      ln[i] = s;
+    }
+    NOC_UNROLL for (int i = 0; i < NX; ++i) { lam[i] = ln[i]; L[(size_t)k * NX + i] = ln[i]; }
+    cost += w.lc[t];
+  }
+  w.cost[b] = cost;                 // total_cost(x, u, bp) (P:142)
+  w.hu[b] = hu;                     // max |Hu| (P:158)
+  const double gn = sqrt(g2);       // ||cu||_F (P:116)
+  w.gnorm[b] = gn;
+  // regularisation fed to the KKT solve: par R += rp*||cu||*I (P:116-118); seq Quu += mu*I (S:51)
+  w.reg[b] = (mode == NOC_MODE_PAR) ? w.rp[b] * gn : w.rp[b];
+  w.inner[b] = 0;
+}
+
+template <int KIND, int NX, int NU>
+__global__ __launch_bounds__(256) void assemble_kernel(noc_family prm, noc_ipm_ws w, int terminal) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = w.N;
+  if (t >= (long long)w.Bt * N) return;
+  const int b = (int)(t / N), k = (int)(t % N);
+  if (w.phase[b] != NOC_PHASE_LINEARIZE) return;
+  Fam<KIND, NX, NU> f(prm);
+  const double bp = w.bp[b];
+  double x[NX], u[NU], lam[NX];
+  gload<NX>(w.x + ((size_t)b * (N + 1) + k) * NX, x);
+  NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = w.u[(size_t)t * NU + j];
+  gload<NX>(w.lam + ((size_t)b * (N + 1) + k + 1) * NX, lam);
+  // Q = cxx + l.fxx ; R = cuu + l.fuu ; M = cxu + l.fxu  (P:35-37), l = lambda_{k+1}
+  double Q[NX * NX], R[NU * NU], M[NX * NU];
+  NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) Q[i * NX + j] = (i == j) ? prm.wx[i] : 0.0;
+  NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int j = 0; j < NU; ++j) R[i * NU + j] = (i == j) ? f.stage_cuu(u, bp, i) : 0.0;
+  NOC_UNROLL for (int i = 0; i < NX * NU; ++i) M[i] = 0.0;
+  f.add_hess_l(x, u, lam, Q, R, M);
+  gstore<NX * NX>(w.Q + (size_t)t * NX * NX, Q);
+  gstore<NU * NU>(w.R + (size_t)t * NU * NU, R);
+  gstore<NX * NU>(w.M + (size_t)t * NX * NU, M);
+  if (terminal == NOC_TERMINAL_STAGE0 && k == 0) gstore<NX * NX>(w.P + (size_t)b * NX * NX, Q);  // P:73
+}
+
+__global__ __launch_bounds__(256) void mark_solve_kernel(noc_ipm_ws w) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= w.Bt) return;
+  const int ph = w.phase[b];
+  if (ph == NOC_PHASE_LINEARIZE) w.phase[b] = NOC_PHASE_SOLVE;
+  w.kkt_active[b] = (ph == NOC_PHASE_DONE) ? 0 : 1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// trial point + Newton / barrier logic: one wave64 per trajectory (4 per 256-thread block)
+NOC_DEV double wave_sum(double v) {
+  NOC_UNROLL for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int KIND, int NX, int NU>
+__global__ __launch_bounds__(256) void trial_kernel(noc_family prm, noc_ipm_ws w, int mode) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= w.Bt || w.phase[b] != NOC_PHASE_SOLVE) return;  // uniform per wave
+  Fam<KIND, NX, NU> f(prm);
+  const int N = w.N;
+  const double bp = w.bp[b];
+  const double* X = w.x + (size_t)b * (N + 1) * NX;
+  const double* DX = w.dx + (size_t)b * (N + 1) * NX;
+  const double* U = w.u + (size_t)b * N * NU;
+  const double* DU = w.du + (size_t)b * N * NU;
+  double csum = 0.0;
+  int ok = 1;
+  for (int k = lane; k < N; k += 64) {
+    double xt[NX], ut[NU];
+    NOC_UNROLL for (int i = 0; i < NX; ++i) xt[i] = X[(size_t)k * NX + i] + DX[(size_t)k * NX + i];
+    NOC_UNROLL for (int j = 0; j < NU; ++j) ut[j] = U[(size_t)k * NU + j] + DU[(size_t)k * NU + j];
+    ok &= f.feasible(ut) ? 1 : 0;
+    csum += f.stage_cost(xt, ut, bp);
+  }
+  if (lane == 0) {
+    double xt[NX];
+    NOC_UNROLL for (int i = 0; i < NX; ++i) xt[i] = X[(size_t)N * NX + i] + DX[(size_t)N * NX + i];
+    csum += f.final_cost(xt);
+  }
+  csum = wave_sum(csum);
+  const bool traj_ok = __all(ok);
+  // new_cost = where(feasible, total_cost(trial), inf)   (P:159-163, S:126-129)
+  const double new_cost = traj_ok ? csum : INFINITY;
+  const double cost = w.cost[b];
+  const double pred = w.pred[b];
+  const bool bwd_ok = w.feasible[b] != 0;
+  const double gain = (new_cost - cost) / pred;           // P:164-165
+  const bool success = (gain > 0.0) && bwd_ok;            // P:166 / S:137
+  double rp = w.rp[b], rinc = w.rinc[b];
+  const double shrink = fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0));
+  rp = success ? rp * shrink : rp * rinc;                 // P:167-171 / S:139-143
+  rinc = success ? 2.0 : 2.0 * rinc;                      // P:172 / S:144
+  bool take, end_iter, stop;
+  int inner = w.inner[b] + 1;
+  if (mode == NOC_MODE_PAR) {
+    rp = fmin(fmax(rp, 1e-16), 1e16);                     // P:173
+    end_iter = success || inner > 500;                    // P:177-182
+    take = end_iter;                                      // the last trial is kept (P:175, P:184)
+    stop = end_iter && (w.hu[b] < 1e-4 || w.it[b] + 1 > 1000);  // P:199-202
+  } else {
+    take = success;                                       // S:145-146
+    end_iter = true;
+    stop = (w.hu[b] < 1e-4) && bwd_ok;                    // S:157-161
+  }
+  if (take) {  // x <- x + dx, u <- u + du
+    double* Xw = w.x + (size_t)b * (N + 1) * NX;
+    double* Uw = w.u + (size_t)b * N * NU;
+    for (int k = lane; k <= N; k += 64) {
+      NOC_UNROLL for (int i = 0; i < NX; ++i) Xw[(size_t)k * NX + i] += DX[(size_t)k * NX + i];
+      if (k < N) NOC_UNROLL for (int j = 0; j < NU; ++j) Uw[(size_t)k * NU + j] += DU[(size_t)k * NU + j];
+    }
+  }
+  if (lane != 0) return;
+  w.kkt_solves[b] += 1;
+  w.inner[b] = inner;
+  int it = w.it[b] + (end_iter ? 1 : 0);
+  int phase;
+  if (stop) {                                             // barrier stage finished
+    w.total_it[b] += it;                                  // P:239 / S:187
+    const double nbp = bp / 5.0;                          // P:238 / S:186
+    w.bp[b] = nbp;
+    it = 0;
+    rp = 1.0;                                             // P:134 / S:110
+    rinc = 2.0;                                           // P:135 / S:111
+    phase = (nbp > 1e-4) ? NOC_PHASE_ROLLOUT : NOC_PHASE_DONE;  // P:243-245
+  } else if (mode == NOC_MODE_PAR) {
+    phase = end_iter ? NOC_PHASE_LINEARIZE : NOC_PHASE_SOLVE;
+  } else {
+    // seq: the next iteration linearises at x (+step if taken); a rejected step leaves x, u
+    // unchanged, so only the regularisation changes (same blocks, cheaper: skip relinearising)
+    phase = success ? NOC_PHASE_LINEARIZE : NOC_PHASE_SOLVE;
+  }
+  w.it[b] = it;
+  w.rp[b] = rp;
+  w.rinc[b] = rinc;
+  if (phase == NOC_PHASE_SOLVE) w.reg[b] = (mode == NOC_MODE_PAR) ? rp * w.gnorm[b] : rp;
+  w.phase[b] = phase;
+}
+
+__global__ __launch_bounds__(256) void init_kernel(noc_ipm_ws w, double bp0) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= w.Bt) return;
+  w.phase[b] = NOC_PHASE_ROLLOUT;
+  w.kkt_active[b] = 1;
+  w.it[b] = 0;
+  w.inner[b] = 0;
+  w.total_it[b] = 0;
+  w.kkt_solves[b] = 0;
+  w.bp[b] = bp0;
+  w.rp[b] = 1.0;
+  w.rinc[b] = 2.0;
+  w.hu[b] = 1.0;
+}
+
+// ------------------------------------------------------------------------------------------------
+template <int KIND, int NX, int NU>
+static hipError_t prepare_t(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                            hipStream_t s) {
+  const int bt_grid = (w.Bt + 255) / 256;
+  const unsigned st_grid = (unsigned)(((long long)w.Bt * w.N + 255) / 256);
+  hipLaunchKernelGGL((rollout_kernel<KIND, NX, NU>), dim3(bt_grid), dim3(256), 0, s, p, w);
+  hipLaunchKernelGGL((linearize_kernel<KIND, NX, NU>), dim3(st_grid), dim3(256), 0, s, p, w);
+  hipLaunchKernelGGL((costate_kernel<KIND, NX, NU>), dim3(bt_grid), dim3(256), 0, s, p, w, mode);
+  hipLaunchKernelGGL((assemble_kernel<KIND, NX, NU>), dim3(st_grid), dim3(256), 0, s, p, w, terminal);
+  hipLaunchKernelGGL(mark_solve_kernel, dim3(bt_grid), dim3(256), 0, s, w);
+  return hipGetLastError();
+}
+
+template <int KIND, int NX, int NU>
+static hipError_t trial_t(const noc_family& p, const noc_ipm_ws& w, int mode, hipStream_t s) {
+  const unsigned grid = (unsigned)((w.Bt + 3) / 4);
+  hipLaunchKernelGGL((trial_kernel<KIND, NX, NU>), dim3(grid), dim3(256), 0, s, p, w, mode);
+  return hipGetLastError();
+}
+
+hipError_t ipm_prepare(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                       hipStream_t s) {
+  switch (p.kind) {
+    case NOC_FAMILY_PENDULUM:
+      if (p.nx == 2 && p.nu == 1) return prepare_t<NOC_FAMILY_PENDULUM, 2, 1>(p, w, mode, terminal, s);
+      break;
+    case NOC_FAMILY_CARTPOLE:
+      if (p.nx == 4 && p.nu == 1) return prepare_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, w, mode, terminal, s);
+      break;
+    case NOC_FAMILY_LINEAR:
+      if (p.nx == 2 && p.nu == 1) return prepare_t<NOC_FAMILY_LINEAR, 2, 1>(p, w, mode, terminal, s);
+      if (p.nx == 8 && p.nu == 4) return prepare_t<NOC_FAMILY_LINEAR, 8, 4>(p, w, mode, terminal, s);
+      break;
+    default: break;
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t ipm_trial(const noc_family& p, const noc_ipm_ws& w, int mode, hipStream_t s) {
+  switch (p.kind) {
+    case NOC_FAMILY_PENDULUM:
+      if (p.nx == 2 && p.nu == 1) return trial_t<NOC_FAMILY_PENDULUM, 2, 1>(p, w, mode, s);
+      break;
+    case NOC_FAMILY_CARTPOLE:
+      if (p.nx == 4 && p.nu == 1) return trial_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, w, mode, s);
+      break;
+    case NOC_FAMILY_LINEAR:
+      if (p.nx == 2 && p.nu == 1) return trial_t<NOC_FAMILY_LINEAR, 2, 1>(p, w, mode, s);
+      if (p.nx == 8 && p.nu == 4) return trial_t<NOC_FAMILY_LINEAR, 8, 4>(p, w, mode, s);
+      break;
+    default: break;
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t ipm_init(const noc_ipm_ws& w, double bp0, hipStream_t s) {
+  hipLaunchKernelGGL(init_kernel, dim3((w.Bt + 255) / 256), dim3(256), 0, s, w, bp0);
+  return hipGetLastError();
+}
+
+bool family_supported(const noc_family& p) {
+  switch (p.kind) {
+    case NOC_FAMILY_PENDULUM: return p.nx == 2 && p.nu == 1;
+    case NOC_FAMILY_CARTPOLE: return p.nx == 4 && p.nu == 1;
+    case NOC_FAMILY_LINEAR: return (p.nx == 2 && p.nu == 1) || (p.nx == 8 && p.nu == 4);
+    default: return false;
+  }
+}
+
+}  // namespace noc

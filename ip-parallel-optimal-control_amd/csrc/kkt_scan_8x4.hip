@@ -1,0 +1,8 @@
+// Instantiation unit of the KKT scan for (nx, nu) = (8, 4); see kkt_scan_impl.h.
+#include "kkt_scan_impl.h"
+
+namespace noc {
+hipError_t kkt_dispatch_8x4(const KKTArgs& a, int lanes, hipStream_t stream) {
+  return dispatch_aff<8, 4>(a, lanes, stream);
+}
+}  // namespace noc

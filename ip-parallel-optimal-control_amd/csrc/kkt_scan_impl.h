@@ -1,0 +1,577 @@
+// Batched parallel-in-time KKT solve of the interior-point Newton step (fp64, gfx950).
+//
+// Replaces paroc.par_bwd_pass + paroc.par_fwd_pass as called by par_Newton
+// (noc/par_interior_point_newton.py:119-123) and examples/linear_mpc_parallel.py:68-69.
+// Mathematically it is the stage-structured KKT solve of seq_interior_point_newton.bwd_pass /
+// fwd_pass (noc/seq_interior_point_newton.py:42-90), computed as an associative scan along the
+// horizon (Saerkkae & Garcia-Fernandez temporal-parallel LQ, the algorithm behind paroc).
+//
+// Mapping (one trajectory per L-lane segment of a wave64; L = 64 is one trajectory per wave):
+//   * lane l of the segment owns the contiguous chunk of stages [start_l, start_l + len_l);
+//   * phase 1  in-chunk element   : the lane folds its stages right-to-left into one scan element
+//                                  (A, b, C, nu, J) with the Riccati-form "prepend" (no R^-1);
+//                                  the segment's last lane starts from the terminal cost.
+//   * phase 2  cross-lane scan    : reverse Hillis-Steele over the L lanes, wave shuffles;
+//                                  afterwards lane l holds the value function at start_l.
+//   * phase 3  in-chunk Riccati   : from the true boundary value (lane l+1's result) the lane runs
+//                                  the sequential Riccati over its chunk -> gains K, d, value S, v,
+//                                  pred (sum dV), feasibility (LDL' pivots > 0), and composes its
+//                                  chunk's closed-loop affine map.
+//   * phase 4  forward scan       : inclusive forward scan of the affine maps (noc/costates.py:6-12
+//                                  combine pattern) gives each lane its start state; the lane then
+//                                  propagates dx, du through its chunk.
+// Conventions: include/noc_hip.h.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "small_linalg.h"
+#include "noc_internal.h"
+
+#ifndef NOC_KKT_WAVES_PER_SIMD
+#define NOC_KKT_WAVES_PER_SIMD 2
+#endif
+
+namespace noc {
+
+template <int NX, int NU>
+struct StageData {
+  Mat<NX, NX> A;
+  Mat<NX, NU> B;
+  Sym<NX> Q;
+  Sym<NU> R;
+  Mat<NX, NU> M;
+  Vec<NU> r;
+  Vec<NX> q;
+  Vec<NX> c;
+};
+
+template <int NX>
+struct Elem {
+  Mat<NX, NX> A;
+  Vec<NX> b;
+  Sym<NX> C;
+  Vec<NX> nu;
+  Sym<NX> J;
+};
+
+template <int NX, int NU, bool AFF>
+NOC_DEV void load_stage(const KKTArgs& a, size_t si, double reg, StageData<NX, NU>& st) {
+  gload<NX * NX>(a.A + si * (NX * NX), st.A.v);
+  gload<NX * NU>(a.Bm + si * (NX * NU), st.B.v);
+  gload_sym<NX>(a.Q + si * (NX * NX), st.Q);
+  gload_sym<NU>(a.R + si * (NU * NU), st.R);
+  NOC_UNROLL for (int i = 0; i < NU; ++i) st.R(i, i) += reg;
+  gload<NX * NU>(a.M + si * (NX * NU), st.M.v);
+  gload<NU>(a.r + si * NU, st.r.v);
+  if constexpr (AFF) {
+    if (a.q) gload<NX>(a.q + si * NX, st.q.v); else set_zero(st.q);
+    if (a.c) gload<NX>(a.c + si * NX, st.c.v); else set_zero(st.c);
+  }
+}
+
+// e <- stage (x) e   (Riccati-form prepend of one stage to the chunk element)
+template <int NX, int NU, bool AFF>
+NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st) {
+  Mat<NX, NX> JA;
+  Mat<NX, NU> JB;
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    NOC_UNROLL for (int j = 0; j < NX; ++j) {
+      double s = 0.0;
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += e.J(i, k) * st.A(k, j);
+      JA(i, j) = s;
+    }
+    NOC_UNROLL for (int j = 0; j < NU; ++j) {
+      double s = 0.0;
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += e.J(i, k) * st.B(k, j);
+      JB(i, j) = s;
+    }
+  }
+  Vec<NX> g;
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    double s = e.nu[i];
+    if constexpr (AFF) { NOC_UNROLL for (int k = 0; k < NX; ++k) s += e.J(i, k) * st.c[k]; }
+    g[i] = s;
+  }
+  Sym<NU> W;
+  NOC_UNROLL for (int i = 0; i < NU; ++i)
+    NOC_UNROLL for (int j = i; j < NU; ++j) {
+      double s = st.R(i, j);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += st.B(k, i) * JB(k, j);
+      W(i, j) = s;
+    }
+  // AB = e.A * B
+  Mat<NX, NU> AB;
+  NOC_UNROLL for (int i = 0; i < NX; ++i)
+    NOC_UNROLL for (int j = 0; j < NU; ++j) {
+      double s = 0.0;
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += e.A(i, k) * st.B(k, j);
+      AB(i, j) = s;
+    }
+  // Y = [Qux | Qu | AB']  (NU x (2NX+1))
+  constexpr int NR = 2 * NX + 1;
+  double Y[NU][NR];
+  Mat<NU, NX> Qux;
+  NOC_UNROLL for (int i = 0; i < NU; ++i) {
+    NOC_UNROLL for (int j = 0; j < NX; ++j) {
+      double s = st.M(j, i);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += JB(k, i) * st.A(k, j);
+      Qux(i, j) = s;
+      Y[i][j] = s;
+    }
+    double s = st.r[i];
+    NOC_UNROLL for (int k = 0; k < NX; ++k) s += st.B(k, i) * g[k];
+    Y[i][NX] = s;
+    NOC_UNROLL for (int t = 0; t < NX; ++t) Y[i][NX + 1 + t] = AB(t, i);
+  }
+  (void)ldl_solve<NU, NR>(W, Y);  // Y <- W^-1 Y   (K = -Y[:, :NX], k = -Y[:, NX])
+  // J <- Q + A' J A + Qux' K ;  nu <- q + A' g + Qux' k
+  Sym<NX> Jn;
+  NOC_UNROLL for (int i = 0; i < NX; ++i)
+    NOC_UNROLL for (int j = i; j < NX; ++j) {
+      double s = st.Q(i, j);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += st.A(k, i) * JA(k, j);
+      NOC_UNROLL for (int t = 0; t < NU; ++t) s -= Qux(t, i) * Y[t][j];
+      Jn(i, j) = s;
+    }
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    double s = AFF ? st.q[i] : 0.0;
+    NOC_UNROLL for (int k = 0; k < NX; ++k) s += st.A(k, i) * g[k];
+    NOC_UNROLL for (int t = 0; t < NU; ++t) s -= Qux(t, i) * Y[t][NX];
+    e.nu[i] = s;
+  }
+  e.J = Jn;
+  // C <- C + AB W^-1 AB'
+  NOC_UNROLL for (int i = 0; i < NX; ++i)
+    NOC_UNROLL for (int j = i; j < NX; ++j) {
+      double s = e.C(i, j);
+      NOC_UNROLL for (int t = 0; t < NU; ++t) s += AB(i, t) * Y[t][NX + 1 + j];
+      e.C(i, j) = s;
+    }
+  // F = A + B K, f = B k + c ;  b <- eA f + b ; A <- eA F
+  Mat<NX, NX> F;
+  Vec<NX> f;
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    NOC_UNROLL for (int j = 0; j < NX; ++j) {
+      double s = st.A(i, j);
+      NOC_UNROLL for (int t = 0; t < NU; ++t) s -= st.B(i, t) * Y[t][j];
+      F(i, j) = s;
+    }
+    double s = AFF ? st.c[i] : 0.0;
+    NOC_UNROLL for (int t = 0; t < NU; ++t) s -= st.B(i, t) * Y[t][NX];
+    f[i] = s;
+  }
+  Mat<NX, NX> An;
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    double sb = e.b[i];
+    NOC_UNROLL for (int k = 0; k < NX; ++k) sb += e.A(i, k) * f[k];
+    e.b[i] = sb;
+    NOC_UNROLL for (int j = 0; j < NX; ++j) {
+      double s = 0.0;
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += e.A(i, k) * F(k, j);
+      An(i, j) = s;
+    }
+  }
+  e.A = An;
+}
+
+// e1 <- e1 (x) e2  (e1 covers the earlier interval, e2 = the partner lane's element, later one).
+// Partner fields arrive in two shuffle batches so that at most one half of e2 is live at a time;
+// lanes without a partner (l + d >= L) get the identity element (I, 0, 0, 0, 0), for which the
+// combine is exact, so the whole segment runs one uniform instruction stream (no divergent
+// ds_bpermute: a shuffle never reads an EXEC-masked lane).
+template <int NX>
+NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L, bool valid) {
+  Sym<NX> J2;
+  Vec<NX> nu2;
+  shfl_down_arr<Sym<NX>::SZ>(e1.J.v, J2.v, d, L);
+  shfl_down_arr<NX>(e1.nu.v, nu2.v, d, L);
+  NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) J2.v[i] = valid ? J2.v[i] : 0.0;
+  NOC_UNROLL for (int i = 0; i < NX; ++i) nu2.v[i] = valid ? nu2.v[i] : 0.0;
+
+  double X[NX][NX];
+  constexpr int NR = 2 * NX + 1;
+  double Y[NX][NR];
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    NOC_UNROLL for (int j = 0; j < NX; ++j) {
+      double s = (i == j) ? 1.0 : 0.0;
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += e1.C(i, k) * J2(k, j);
+      X[i][j] = s;
+      Y[i][j] = e1.A(i, j);
+      Y[i][NX + 1 + j] = e1.C(i, j);
+    }
+    double s = e1.b[i];
+    NOC_UNROLL for (int k = 0; k < NX; ++k) s -= e1.C(i, k) * nu2[k];
+    Y[i][NX] = s;
+  }
+  //  J2A1 = J2 A1,  w = nu2 + J2 b1   (e1.A, e1.b are still the pre-combine values)
+  Mat<NX, NX> J2A1;
+  Vec<NX> w;
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    double sw = nu2[i];
+    NOC_UNROLL for (int k = 0; k < NX; ++k) sw += J2(i, k) * e1.b[k];
+    w[i] = sw;
+    NOC_UNROLL for (int j = 0; j < NX; ++j) {
+      double s = 0.0;
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += J2(i, k) * e1.A(k, j);
+      J2A1(i, j) = s;
+    }
+  }
+  lu_pp_solve<NX, NR>(X, Y);  // Y = [TA | Tb | TC],  T = (I + C1 J2)^-1
+  // J = J1 + TA' J2 A1 ; nu = nu1 + TA' w
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    NOC_UNROLL for (int j = i; j < NX; ++j) {
+      double s = e1.J(i, j);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * J2A1(k, j);
+      e1.J(i, j) = s;
+    }
+    double s = e1.nu[i];
+    NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * w[k];
+    e1.nu[i] = s;
+  }
+  // second batch: partner's A, b, C (not yet modified by any lane at this level)
+  Mat<NX, NX> A2;
+  Vec<NX> b2;
+  Sym<NX> C2;
+  shfl_down_arr<NX * NX>(e1.A.v, A2.v, d, L);
+  shfl_down_arr<NX>(e1.b.v, b2.v, d, L);
+  shfl_down_arr<Sym<NX>::SZ>(e1.C.v, C2.v, d, L);
+  NOC_UNROLL for (int i = 0; i < NX; ++i)
+    NOC_UNROLL for (int j = 0; j < NX; ++j) A2(i, j) = valid ? A2(i, j) : (i == j ? 1.0 : 0.0);
+  NOC_UNROLL for (int i = 0; i < NX; ++i) b2.v[i] = valid ? b2.v[i] : 0.0;
+  NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) C2.v[i] = valid ? C2.v[i] : 0.0;
+  // A = A2 TA ; b = A2 Tb + b2 ; C = A2 TC A2' + C2
+  Mat<NX, NX> T2;  // A2 * TC
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    double sb = b2[i];
+    NOC_UNROLL for (int k = 0; k < NX; ++k) sb += A2(i, k) * Y[k][NX];
+    e1.b[i] = sb;
+    NOC_UNROLL for (int j = 0; j < NX; ++j) {
+      double sa = 0.0, st = 0.0;
+      NOC_UNROLL for (int k = 0; k < NX; ++k) {
+        sa += A2(i, k) * Y[k][j];
+        st += A2(i, k) * Y[k][NX + 1 + j];
+      }
+      e1.A(i, j) = sa;
+      T2(i, j) = st;
+    }
+  }
+  NOC_UNROLL for (int i = 0; i < NX; ++i)
+    NOC_UNROLL for (int j = i; j < NX; ++j) {
+      double s = C2(i, j);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += T2(i, k) * A2(j, k);
+      e1.C(i, j) = s;
+    }
+}
+
+template <int NX, int NU, int L, bool AFF>
+__global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int traj = tid / L;
+  const int l = tid % L;
+  if (traj >= a.B) return;                     // uniform over the segment
+  if (a.active && a.active[traj] == 0) return;  // uniform over the segment
+  const int N = a.N;
+  const int base = N / L, rem = N % L;
+  const int len = base + (l < rem ? 1 : 0);
+  const int start = l * base + (l < rem ? l : rem);
+  const bool last = (l == L - 1);
+  const double reg = a.reg ? a.reg[traj] : 0.0;
+  const size_t tN = (size_t)traj * N;
+
+
+  Mat<NX, NX> Phi;
+  Vec<NX> phi;
+  if (a.mode != MODE_FWD) {
+    // ---------------- phase 1: in-chunk element ----------------
+    Elem<NX> e;
+    set_zero(e.b);
+    set_zero(e.C);
+    if (last) {  // terminal cost (0, 0, 0, p, P)
+      set_zero(e.A);
+      set_zero(e.nu);
+      gload_sym<NX>(a.P + (size_t)traj * NX * NX, e.J);
+      if constexpr (AFF) { if (a.p) gload<NX>(a.p + (size_t)traj * NX, e.nu.v); }
+    } else {
+      set_identity(e.A);
+      set_zero(e.nu);
+      set_zero(e.J);
+    }
+    for (int s = start + len - 1; s >= start; --s) {
+      StageData<NX, NU> st;
+      load_stage<NX, NU, AFF>(a, tN + s, reg, st);
+      prepend<NX, NU, AFF>(e, st);
+    }
+    // ---------------- phase 2: reverse Hillis-Steele across lanes ----------------
+#pragma unroll 1
+    for (int d = 1; d < L; d <<= 1) combine_shfl<NX>(e, d, L, l + d < L);
+    // ---------------- phase 3: in-chunk Riccati from the true boundary ----------------
+    Sym<NX> S;
+    Vec<NX> v;
+    shfl_down_arr<Sym<NX>::SZ>(e.J.v, S.v, 1, L);
+    shfl_down_arr<NX>(e.nu.v, v.v, 1, L);
+    if (last) {  // boundary of the last chunk: the terminal cost itself (reloaded, not kept live)
+      gload_sym<NX>(a.P + (size_t)traj * NX * NX, S);
+      set_zero(v);
+      if constexpr (AFF) { if (a.p) gload<NX>(a.p + (size_t)traj * NX, v.v); }
+      if (a.S) gstore_sym<NX>(a.S + (tN + traj + N) * (NX * NX), S);
+      if (a.v) gstore<NX>(a.v + (tN + traj + N) * NX, v.v);
+    }
+    set_identity(Phi);
+    set_zero(phi);
+    double pred = 0.0;
+    int feas = 1;
+    for (int s = start + len - 1; s >= start; --s) {
+      StageData<NX, NU> st;
+      load_stage<NX, NU, AFF>(a, tN + s, reg, st);
+      Mat<NX, NX> SA;
+      Mat<NX, NU> SB;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        NOC_UNROLL for (int j = 0; j < NX; ++j) {
+          double t = 0.0;
+          NOC_UNROLL for (int k = 0; k < NX; ++k) t += S(i, k) * st.A(k, j);
+          SA(i, j) = t;
+        }
+        NOC_UNROLL for (int j = 0; j < NU; ++j) {
+          double t = 0.0;
+          NOC_UNROLL for (int k = 0; k < NX; ++k) t += S(i, k) * st.B(k, j);
+          SB(i, j) = t;
+        }
+      }
+      Vec<NX> g;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        double t = v[i];
+        if constexpr (AFF) { NOC_UNROLL for (int k = 0; k < NX; ++k) t += S(i, k) * st.c[k]; }
+        g[i] = t;
+      }
+      Sym<NU> Quu;
+      NOC_UNROLL for (int i = 0; i < NU; ++i)
+        NOC_UNROLL for (int j = i; j < NU; ++j) {
+          double t = st.R(i, j);
+          NOC_UNROLL for (int k = 0; k < NX; ++k) t += st.B(k, i) * SB(k, j);
+          Quu(i, j) = t;
+        }
+      constexpr int NR = NX + 1;
+      double Y[NU][NR];
+      Mat<NU, NX> Qux;
+      Vec<NU> Qu;
+      NOC_UNROLL for (int i = 0; i < NU; ++i) {
+        NOC_UNROLL for (int j = 0; j < NX; ++j) {
+          double t = st.M(j, i);
+          NOC_UNROLL for (int k = 0; k < NX; ++k) t += SB(k, i) * st.A(k, j);
+          Qux(i, j) = t;
+          Y[i][j] = t;
+        }
+        double t = st.r[i];
+        NOC_UNROLL for (int k = 0; k < NX; ++k) t += st.B(k, i) * g[k];
+        Qu[i] = t;
+        Y[i][NX] = t;
+      }
+      feas &= ldl_solve<NU, NR>(Quu, Y) ? 1 : 0;
+      // K = -Y[:, :NX], k = -Y[:, NX]
+      double Kk[NU * (NX + 1)];
+      NOC_UNROLL for (int i = 0; i < NU; ++i) {
+        NOC_UNROLL for (int j = 0; j < NX; ++j) Kk[i * NX + j] = -Y[i][j];
+        Kk[NU * NX + i] = -Y[i][NX];
+      }
+      gstore<NU * NX>(a.K + (tN + s) * (NU * NX), Kk);
+      gstore<NU>(a.d + (tN + s) * NU, Kk + NU * NX);
+      // dV = k'Qu + 1/2 k'Quu k   (noc/seq_interior_point_newton.py:63)
+      NOC_UNROLL for (int i = 0; i < NU; ++i) {
+        const double ki = Kk[NU * NX + i];
+        double qk = 0.0;
+        NOC_UNROLL for (int j = 0; j < NU; ++j) qk += Quu(i, j) * Kk[NU * NX + j];
+        pred += ki * Qu[i] + 0.5 * ki * qk;
+      }
+      // S <- Q + A' S A + Qux' K ; v <- q + A' g + Qux' k
+      Sym<NX> Sn;
+      NOC_UNROLL for (int i = 0; i < NX; ++i)
+        NOC_UNROLL for (int j = i; j < NX; ++j) {
+          double t = st.Q(i, j);
+          NOC_UNROLL for (int k = 0; k < NX; ++k) t += st.A(k, i) * SA(k, j);
+          NOC_UNROLL for (int u = 0; u < NU; ++u) t += Qux(u, i) * Kk[u * NX + j];
+          Sn(i, j) = t;
+        }
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        double t = AFF ? st.q[i] : 0.0;
+        NOC_UNROLL for (int k = 0; k < NX; ++k) t += st.A(k, i) * g[k];
+        NOC_UNROLL for (int u = 0; u < NU; ++u) t += Qux(u, i) * Kk[NU * NX + u];
+        v[i] = t;
+      }
+      S = Sn;
+      if (a.S) gstore_sym<NX>(a.S + (tN + traj + s) * (NX * NX), S);
+      if (a.v) gstore<NX>(a.v + (tN + traj + s) * NX, v.v);
+      // closed-loop map of this stage: F = A + B K, f = B k + c ; phi += Phi f ; Phi <- Phi F
+      Mat<NX, NX> F;
+      Vec<NX> f;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        NOC_UNROLL for (int j = 0; j < NX; ++j) {
+          double t = st.A(i, j);
+          NOC_UNROLL for (int u = 0; u < NU; ++u) t += st.B(i, u) * Kk[u * NX + j];
+          F(i, j) = t;
+        }
+        double t = AFF ? st.c[i] : 0.0;
+        NOC_UNROLL for (int u = 0; u < NU; ++u) t += st.B(i, u) * Kk[NU * NX + u];
+        f[i] = t;
+      }
+      Mat<NX, NX> Pn;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        double t = phi[i];
+        NOC_UNROLL for (int k = 0; k < NX; ++k) t += Phi(i, k) * f[k];
+        phi[i] = t;
+        NOC_UNROLL for (int j = 0; j < NX; ++j) {
+          double u = 0.0;
+          NOC_UNROLL for (int k = 0; k < NX; ++k) u += Phi(i, k) * F(k, j);
+          Pn(i, j) = u;
+        }
+      }
+      Phi = Pn;
+    }
+    // segment reductions: pred = sum, feasible = and
+    NOC_UNROLL for (int off = L / 2; off > 0; off >>= 1) {
+      pred += __shfl_xor(pred, off, L);
+      feas &= __shfl_xor(feas, off, L);
+    }
+    if (l == 0) {
+      if (a.pred) a.pred[traj] = pred;
+      if (a.feasible) a.feasible[traj] = feas;
+    }
+    if (a.mode == MODE_BWD) return;
+  } else {
+    // MODE_FWD: gains are inputs; compose the chunk's closed-loop map from A, B, K, d
+    set_identity(Phi);
+    set_zero(phi);
+    for (int s = start + len - 1; s >= start; --s) {
+      Mat<NX, NX> A;
+      Mat<NX, NU> Bm;
+      double Kk[NU * (NX + 1)];
+      gload<NX * NX>(a.A + (tN + s) * (NX * NX), A.v);
+      gload<NX * NU>(a.Bm + (tN + s) * (NX * NU), Bm.v);
+      gload<NU * NX>(a.K + (tN + s) * (NU * NX), Kk);
+      gload<NU>(a.d + (tN + s) * NU, Kk + NU * NX);
+      Vec<NX> cc;
+      set_zero(cc);
+      if constexpr (AFF) { if (a.c) gload<NX>(a.c + (tN + s) * NX, cc.v); }
+      Mat<NX, NX> F;
+      Vec<NX> f;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        NOC_UNROLL for (int j = 0; j < NX; ++j) {
+          double t = A(i, j);
+          NOC_UNROLL for (int u = 0; u < NU; ++u) t += Bm(i, u) * Kk[u * NX + j];
+          F(i, j) = t;
+        }
+        double t = cc[i];
+        NOC_UNROLL for (int u = 0; u < NU; ++u) t += Bm(i, u) * Kk[NU * NX + u];
+        f[i] = t;
+      }
+      Mat<NX, NX> Pn;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        double t = phi[i];
+        NOC_UNROLL for (int k = 0; k < NX; ++k) t += Phi(i, k) * f[k];
+        phi[i] = t;
+        NOC_UNROLL for (int j = 0; j < NX; ++j) {
+          double u = 0.0;
+          NOC_UNROLL for (int k = 0; k < NX; ++k) u += Phi(i, k) * F(k, j);
+          Pn(i, j) = u;
+        }
+      }
+      Phi = Pn;
+    }
+  }
+
+  // ---------------- phase 4: forward affine scan + chunk propagation ----------------
+  Vec<NX> x0;
+  set_zero(x0);
+  if (a.x0) gload<NX>(a.x0 + (size_t)traj * NX, x0.v);
+  if (l == 0) {
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      double t = phi[i];
+      NOC_UNROLL for (int k = 0; k < NX; ++k) t += Phi(i, k) * x0[k];
+      phi[i] = t;
+    }
+    set_zero(Phi);
+  }
+#pragma unroll 1
+  for (int d = 1; d < L; d <<= 1) {
+    Mat<NX, NX> oP;
+    Vec<NX> op;
+    shfl_up_arr<NX * NX>(Phi.v, oP.v, d, L);
+    shfl_up_arr<NX>(phi.v, op.v, d, L);
+    const bool valid = l >= d;  // identity map for lanes without a predecessor at this level
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      op[i] = valid ? op[i] : 0.0;
+      NOC_UNROLL for (int j = 0; j < NX; ++j) oP(i, j) = valid ? oP(i, j) : (i == j ? 1.0 : 0.0);
+    }
+    Mat<NX, NX> Pn;
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      double t = phi[i];
+      NOC_UNROLL for (int k = 0; k < NX; ++k) t += Phi(i, k) * op[k];
+      phi[i] = t;
+      NOC_UNROLL for (int j = 0; j < NX; ++j) {
+        double u = 0.0;
+        NOC_UNROLL for (int k = 0; k < NX; ++k) u += Phi(i, k) * oP(k, j);
+        Pn(i, j) = u;
+      }
+    }
+    Phi = Pn;
+  }
+  Vec<NX> x;
+  shfl_up_arr<NX>(phi.v, x.v, 1, L);
+  if (l == 0) x = x0;
+  for (int s = start; s < start + len; ++s) {
+    Mat<NX, NX> A;
+    Mat<NX, NU> Bm;
+    double Kk[NU * (NX + 1)];
+    gload<NX * NX>(a.A + (tN + s) * (NX * NX), A.v);
+    gload<NX * NU>(a.Bm + (tN + s) * (NX * NU), Bm.v);
+    gload<NU * NX>(a.K + (tN + s) * (NU * NX), Kk);
+    gload<NU>(a.d + (tN + s) * NU, Kk + NU * NX);
+    Vec<NU> u;
+    NOC_UNROLL for (int i = 0; i < NU; ++i) {
+      double t = Kk[NU * NX + i];
+      NOC_UNROLL for (int k = 0; k < NX; ++k) t += Kk[i * NX + k] * x[k];
+      u[i] = t;
+    }
+    if (a.dx) gstore<NX>(a.dx + (tN + traj + s) * NX, x.v);
+    if (a.du) gstore<NU>(a.du + (tN + s) * NU, u.v);
+    Vec<NX> xn;
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      double t = 0.0;
+      if constexpr (AFF) { if (a.c) t = a.c[(tN + s) * NX + i]; }
+      NOC_UNROLL for (int k = 0; k < NX; ++k) t += A(i, k) * x[k];
+      NOC_UNROLL for (int j = 0; j < NU; ++j) t += Bm(i, j) * u[j];
+      xn[i] = t;
+    }
+    x = xn;
+  }
+  if (last && a.dx) gstore<NX>(a.dx + (tN + traj + N) * NX, x.v);
+}
+
+// ---------------------------------------------------------------------------------------------
+template <int NX, int NU, int L, bool AFF>
+static hipError_t launch_kkt(const KKTArgs& a, hipStream_t stream) {
+  const long long threads = (long long)a.B * L;
+  const int block = 256;
+  const unsigned grid = (unsigned)((threads + block - 1) / block);
+  hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF>), dim3(grid), dim3(block), 0, stream, a);
+  return hipGetLastError();
+}
+
+template <int NX, int NU, bool AFF>
+static hipError_t dispatch_lanes(const KKTArgs& a, int lanes, hipStream_t stream) {
+  switch (lanes) {
+    case 64: return launch_kkt<NX, NU, 64, AFF>(a, stream);
+    case 32: return launch_kkt<NX, NU, 32, AFF>(a, stream);
+    case 16: return launch_kkt<NX, NU, 16, AFF>(a, stream);
+    case 8: return launch_kkt<NX, NU, 8, AFF>(a, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int NX, int NU>
+static hipError_t dispatch_aff(const KKTArgs& a, int lanes, hipStream_t stream) {
+  const bool aff = a.q || a.c || a.p;
+  return aff ? dispatch_lanes<NX, NU, true>(a, lanes, stream)
+             : dispatch_lanes<NX, NU, false>(a, lanes, stream);
+}
+
+}  // namespace noc

@@ -1,0 +1,203 @@
+// extern "C" entry points of libnoc_hip.so (declared in include/noc_hip.h).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/noc_hip.h"
+#include "noc_internal.h"
+
+namespace {
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int check_ptr(const void* p, const char* name, bool required) {
+  if (!p) return required ? fail(-2, std::string("required pointer is NULL: ") + name) : 0;
+  if (!aligned16(p)) return fail(-3, std::string("pointer not 16-byte aligned: ") + name);
+  return 0;
+}
+
+int hip_status(hipError_t e, const char* where) {
+  if (e == hipSuccess) return 0;
+  return fail(-10, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+int check_dims(int nx, int nu, int N, int B, int lanes) {
+  if (!noc::kkt_supported(nx, nu))
+    return fail(-1, "unsupported (nx, nu) = (" + std::to_string(nx) + ", " + std::to_string(nu) +
+                        "); supported: (2,1) (4,1) (8,4)");
+  if (N < 1) return fail(-1, "horizon N must be >= 1");
+  if (B < 0) return fail(-1, "batch B must be >= 0");
+  if (lanes != 0 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64)
+    return fail(-1, "lanes must be 0, 8, 16, 32 or 64");
+  return 0;
+}
+}  // namespace
+
+namespace noc {
+bool kkt_supported(int nx, int nu) {
+  return (nx == 2 && nu == 1) || (nx == 4 && nu == 1) || (nx == 8 && nu == 4);
+}
+
+hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t stream) {
+  if (nx == 2 && nu == 1) return kkt_dispatch_2x1(a, lanes, stream);
+  if (nx == 4 && nu == 1) return kkt_dispatch_4x1(a, lanes, stream);
+  if (nx == 8 && nu == 4) return kkt_dispatch_8x4(a, lanes, stream);
+  return hipErrorInvalidValue;
+}
+
+int kkt_default_lanes(int nx, int nu, int N) {
+  (void)nx;
+  (void)nu;
+  (void)N;
+  return 64;
+}
+}  // namespace noc
+
+extern "C" {
+
+int noc_abi_version(void) { return NOC_ABI_VERSION; }
+const char* noc_last_error(void) { return g_last_error.c_str(); }
+int noc_kkt_supported(int nx, int nu) { return noc::kkt_supported(nx, nu) ? 1 : 0; }
+int noc_kkt_default_lanes(int nx, int nu, int N) { return noc::kkt_default_lanes(nx, nu, N); }
+
+static int kkt_common(int mode, int nx, int nu, int N, int B, int lanes, const double* A,
+                      const double* Bm, const double* Q, const double* R, const double* M,
+                      const double* r, const double* q, const double* c, const double* P,
+                      const double* p, const double* x0, const double* reg, const int* active,
+                      double* dx, double* du, double* pred, int* feasible, double* K, double* d,
+                      double* S, double* v, void* stream) {
+  int rc = check_dims(nx, nu, N, B, lanes);
+  if (rc) return rc;
+  const bool bwd = mode != noc::MODE_FWD;
+  const bool fwd = mode != noc::MODE_BWD;
+  if ((rc = check_ptr(A, "A", true))) return rc;
+  if ((rc = check_ptr(Bm, "B", true))) return rc;
+  if ((rc = check_ptr(Q, "Q", bwd))) return rc;
+  if ((rc = check_ptr(R, "R", bwd))) return rc;
+  if ((rc = check_ptr(M, "M", bwd))) return rc;
+  if ((rc = check_ptr(r, "r", bwd))) return rc;
+  if ((rc = check_ptr(P, "P", bwd))) return rc;
+  if ((rc = check_ptr(q, "q", false))) return rc;
+  if ((rc = check_ptr(c, "c", false))) return rc;
+  if ((rc = check_ptr(p, "p", false))) return rc;
+  if ((rc = check_ptr(x0, "x0", false))) return rc;
+  if ((rc = check_ptr(K, "K", true))) return rc;
+  if ((rc = check_ptr(d, "d", true))) return rc;
+  if ((rc = check_ptr(S, "S", false))) return rc;
+  if ((rc = check_ptr(v, "v", false))) return rc;
+  if ((rc = check_ptr(dx, "dx", false))) return rc;
+  if ((rc = check_ptr(du, "du", false))) return rc;
+  if (reg && (reinterpret_cast<uintptr_t>(reg) & 7u)) return fail(-3, "reg not 8-byte aligned");
+  if (B == 0) return 0;
+  noc::KKTArgs a{};
+  a.N = N;
+  a.B = B;
+  a.mode = mode;
+  a.A = A; a.Bm = Bm; a.Q = Q; a.R = R; a.M = M; a.r = r; a.q = q; a.c = c;
+  a.P = P; a.p = p; a.x0 = x0; a.reg = reg; a.active = active;
+  a.dx = dx; a.du = du; a.pred = pred; a.K = K; a.d = d; a.S = S; a.v = v;
+  a.feasible = feasible;
+  (void)bwd;
+  (void)fwd;
+  const int L = lanes ? lanes : noc::kkt_default_lanes(nx, nu, N);
+  return hip_status(noc::kkt_dispatch(nx, nu, a, L, static_cast<hipStream_t>(stream)),
+                    "kkt_scan launch");
+}
+
+int noc_kkt_solve(int nx, int nu, int N, int B, int lanes, const double* A, const double* Bm,
+                  const double* Q, const double* R, const double* M, const double* r,
+                  const double* q, const double* c, const double* P, const double* p,
+                  const double* x0, const double* reg, const int* active, double* dx, double* du,
+                  double* pred, int* feasible, double* K, double* d, double* S, double* v,
+                  void* stream) {
+  return kkt_common(noc::MODE_FULL, nx, nu, N, B, lanes, A, Bm, Q, R, M, r, q, c, P, p, x0, reg,
+                    active, dx, du, pred, feasible, K, d, S, v, stream);
+}
+
+int noc_par_bwd_pass(int nx, int nu, int N, int B, int lanes, const double* A, const double* Bm,
+                     const double* Q, const double* R, const double* M, const double* r,
+                     const double* q, const double* c, const double* P, const double* p,
+                     const double* reg, const int* active, double* K, double* d, double* S,
+                     double* v, double* pred, int* feasible, void* stream) {
+  return kkt_common(noc::MODE_BWD, nx, nu, N, B, lanes, A, Bm, Q, R, M, r, q, c, P, p, nullptr,
+                    reg, active, nullptr, nullptr, pred, feasible, K, d, S, v, stream);
+}
+
+int noc_par_fwd_pass(int nx, int nu, int N, int B, int lanes, const double* A, const double* Bm,
+                     const double* c, const double* x0, const double* K, const double* d,
+                     const int* active, double* du, double* dx, void* stream) {
+  return kkt_common(noc::MODE_FWD, nx, nu, N, B, lanes, A, Bm, nullptr, nullptr, nullptr,
+                    nullptr, nullptr, c, nullptr, nullptr, x0, nullptr, active, dx, du, nullptr,
+                    nullptr, const_cast<double*>(K), const_cast<double*>(d), nullptr, nullptr,
+                    stream);
+}
+
+int noc_family_supported(const noc_family* fam) {
+  return (fam && noc::family_supported(*fam)) ? 1 : 0;
+}
+
+static int check_ipm(const noc_family* fam, const noc_ipm_ws* ws) {
+  if (!ws) return fail(-2, "workspace is NULL");
+  if (ws->Bt < 0 || ws->N < 1) return fail(-1, "workspace dims: need Bt >= 0, N >= 1");
+  if (fam && !noc::family_supported(*fam))
+    return fail(-1, "unsupported problem family (kind/nx/nu)");
+  const void* req[] = {ws->x, ws->u, ws->x0, ws->A, ws->B, ws->Q, ws->R, ws->M, ws->r, ws->P,
+                       ws->cx, ws->cu, ws->lc, ws->lam, ws->dx, ws->du, ws->pred, ws->K, ws->d,
+                       ws->feasible, ws->phase, ws->kkt_active, ws->it, ws->inner, ws->total_it,
+                       ws->kkt_solves, ws->bp, ws->rp, ws->rinc, ws->cost, ws->hu, ws->gnorm,
+                       ws->reg};
+  for (const void* p : req)
+    if (!p) return fail(-2, "a required workspace pointer is NULL");
+  return 0;
+}
+
+int noc_ipm_init(const noc_ipm_ws* ws, double bp0, void* stream) {
+  int rc = check_ipm(nullptr, ws);
+  if (rc) return rc;
+  if (ws->Bt == 0) return 0;
+  return hip_status(noc::ipm_init(*ws, bp0, static_cast<hipStream_t>(stream)), "ipm_init");
+}
+
+int noc_ipm_prepare(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal,
+                    void* stream) {
+  if (!fam) return fail(-2, "family is NULL");
+  int rc = check_ipm(fam, ws);
+  if (rc) return rc;
+  if (mode != NOC_MODE_PAR && mode != NOC_MODE_SEQ) return fail(-1, "bad mode");
+  if (terminal != NOC_TERMINAL_FINAL_COST && terminal != NOC_TERMINAL_STAGE0)
+    return fail(-1, "bad terminal option");
+  if (ws->Bt == 0) return 0;
+  return hip_status(noc::ipm_prepare(*fam, *ws, mode, terminal, static_cast<hipStream_t>(stream)),
+                    "ipm_prepare");
+}
+
+int noc_ipm_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* stream) {
+  if (!fam) return fail(-2, "family is NULL");
+  int rc = check_ipm(fam, ws);
+  if (rc) return rc;
+  if (mode != NOC_MODE_PAR && mode != NOC_MODE_SEQ) return fail(-1, "bad mode");
+  if (ws->Bt == 0) return 0;
+  return hip_status(noc::ipm_trial(*fam, *ws, mode, static_cast<hipStream_t>(stream)), "ipm_trial");
+}
+
+int noc_ipm_step(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, int lanes,
+                 void* stream) {
+  int rc = noc_ipm_prepare(fam, ws, mode, terminal, stream);
+  if (rc) return rc;
+  rc = noc_kkt_solve(fam->nx, fam->nu, ws->N, ws->Bt, lanes, ws->A, ws->B, ws->Q, ws->R, ws->M,
+                     ws->r, nullptr, nullptr, ws->P, nullptr, nullptr, ws->reg, ws->kkt_active,
+                     ws->dx, ws->du, ws->pred, ws->feasible, ws->K, ws->d, nullptr, nullptr,
+                     stream);
+  if (rc) return rc;
+  return noc_ipm_trial(fam, ws, mode, stream);
+}
+
+}  // extern "C"

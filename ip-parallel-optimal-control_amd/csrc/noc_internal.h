@@ -1,0 +1,33 @@
+// Internal (non-ABI) declarations shared by the HIP translation units of libnoc_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/noc_hip.h"
+
+namespace noc {
+
+enum KKTMode : int { MODE_FULL = 0, MODE_BWD = 1, MODE_FWD = 2 };
+
+// Kernel argument block of the KKT scan (passed by value).  Layouts: include/noc_hip.h.
+struct KKTArgs {
+  int N, B, mode;
+  const double *A, *Bm, *Q, *R, *M, *r, *q, *c, *P, *p, *x0, *reg;
+  const int* active;
+  double *dx, *du, *pred, *K, *d, *S, *v;
+  int* feasible;
+};
+
+hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t stream);
+hipError_t kkt_dispatch_2x1(const KKTArgs& a, int lanes, hipStream_t stream);
+hipError_t kkt_dispatch_4x1(const KKTArgs& a, int lanes, hipStream_t stream);
+hipError_t kkt_dispatch_8x4(const KKTArgs& a, int lanes, hipStream_t stream);
+bool kkt_supported(int nx, int nu);
+int kkt_default_lanes(int nx, int nu, int N);
+
+hipError_t ipm_prepare(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                       hipStream_t s);
+hipError_t ipm_trial(const noc_family& p, const noc_ipm_ws& w, int mode, hipStream_t s);
+hipError_t ipm_init(const noc_ipm_ws& w, double bp0, hipStream_t s);
+bool family_supported(const noc_family& p);
+
+}  // namespace noc

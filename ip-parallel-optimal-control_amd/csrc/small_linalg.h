@@ -1,0 +1,191 @@
+// Register-resident small dense linear algebra for the gfx950 KKT scan kernels (fp64).
+//
+// Every loop is fully unrolled over compile-time extents, so all matrix entries live in VGPRs
+// (runtime-indexed register arrays would spill to scratch: cdna_hip_programming.md §5.4 rule 20).
+// Symmetric matrices are stored packed (upper triangle, row-major) to cut VGPRs and shuffles.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace noc {
+
+#define NOC_DEV __device__ __forceinline__
+#define NOC_UNROLL _Pragma("unroll")
+
+template <int R, int C>
+struct Mat {
+  double v[R * C];
+  NOC_DEV double& operator()(int i, int j) { return v[i * C + j]; }
+  NOC_DEV double operator()(int i, int j) const { return v[i * C + j]; }
+};
+
+template <int N>
+struct Vec {
+  double v[N];
+  NOC_DEV double& operator[](int i) { return v[i]; }
+  NOC_DEV double operator[](int i) const { return v[i]; }
+};
+
+template <int N>
+struct Sym {
+  static constexpr int SZ = N * (N + 1) / 2;
+  double v[SZ];
+  static NOC_DEV constexpr int idx(int i, int j) {
+    return i <= j ? i * N - (i * (i - 1)) / 2 + (j - i) : j * N - (j * (j - 1)) / 2 + (i - j);
+  }
+  NOC_DEV double& operator()(int i, int j) { return v[idx(i, j)]; }
+  NOC_DEV double operator()(int i, int j) const { return v[idx(i, j)]; }
+};
+
+// ---------------------------------------------------------------------------------------------
+// fills
+template <int R, int C>
+NOC_DEV void set_zero(Mat<R, C>& m) { NOC_UNROLL for (int i = 0; i < R * C; ++i) m.v[i] = 0.0; }
+template <int N>
+NOC_DEV void set_zero(Vec<N>& m) { NOC_UNROLL for (int i = 0; i < N; ++i) m.v[i] = 0.0; }
+template <int N>
+NOC_DEV void set_zero(Sym<N>& m) { NOC_UNROLL for (int i = 0; i < Sym<N>::SZ; ++i) m.v[i] = 0.0; }
+template <int N>
+NOC_DEV void set_identity(Mat<N, N>& m) {
+  NOC_UNROLL for (int i = 0; i < N; ++i) NOC_UNROLL for (int j = 0; j < N; ++j) m(i, j) = (i == j) ? 1.0 : 0.0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// global loads (16-B vector loads when the element count is even; the host checks alignment)
+template <int CNT>
+NOC_DEV void gload(const double* __restrict__ src, double* dst) {
+  if constexpr (CNT % 2 == 0) {
+    const double2* s2 = reinterpret_cast<const double2*>(src);
+    NOC_UNROLL for (int i = 0; i < CNT / 2; ++i) {
+      double2 t = s2[i];
+      dst[2 * i] = t.x;
+      dst[2 * i + 1] = t.y;
+    }
+  } else {
+    NOC_UNROLL for (int i = 0; i < CNT; ++i) dst[i] = src[i];
+  }
+}
+template <int CNT>
+NOC_DEV void gstore(double* __restrict__ dst, const double* src) {
+  if constexpr (CNT % 2 == 0) {
+    double2* d2 = reinterpret_cast<double2*>(dst);
+    NOC_UNROLL for (int i = 0; i < CNT / 2; ++i) d2[i] = make_double2(src[2 * i], src[2 * i + 1]);
+  } else {
+    NOC_UNROLL for (int i = 0; i < CNT; ++i) dst[i] = src[i];
+  }
+}
+
+// load a full row-major N x N matrix and symmetrise it into packed storage
+template <int N>
+NOC_DEV void gload_sym(const double* __restrict__ src, Sym<N>& S) {
+  double t[N * N];
+  gload<N * N>(src, t);
+  NOC_UNROLL for (int i = 0; i < N; ++i)
+    NOC_UNROLL for (int j = i; j < N; ++j) S(i, j) = (i == j) ? t[i * N + i] : 0.5 * (t[i * N + j] + t[j * N + i]);
+}
+template <int N>
+NOC_DEV void gstore_sym(double* __restrict__ dst, const Sym<N>& S) {
+  double t[N * N];
+  NOC_UNROLL for (int i = 0; i < N; ++i) NOC_UNROLL for (int j = 0; j < N; ++j) t[i * N + j] = S(i, j);
+  gstore<N * N>(dst, t);
+}
+
+// ---------------------------------------------------------------------------------------------
+// wave shuffles of whole register blocks (ds_bpermute under the hood, segment width W)
+NOC_DEV double shfl_down_d(double x, int d, int w) { return __shfl_down(x, (unsigned)d, w); }
+NOC_DEV double shfl_up_d(double x, int d, int w) { return __shfl_up(x, (unsigned)d, w); }
+
+template <int CNT>
+NOC_DEV void shfl_down_arr(const double* src, double* dst, int d, int w) {
+  NOC_UNROLL for (int i = 0; i < CNT; ++i) dst[i] = shfl_down_d(src[i], d, w);
+}
+template <int CNT>
+NOC_DEV void shfl_up_arr(const double* src, double* dst, int d, int w) {
+  NOC_UNROLL for (int i = 0; i < CNT; ++i) dst[i] = shfl_up_d(src[i], d, w);
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDL' factorisation + solve of a small symmetric system (no pivoting).  Returns true iff the
+// matrix is positive definite (all D > 0, Sylvester), which is the eigh(Quu) > 0 test of
+// noc/seq_interior_point_newton.py:52-53.  Y (N x NR) is overwritten by W^{-1} Y.
+template <int N, int NR>
+NOC_DEV bool ldl_solve(const Sym<N>& W, double (&Y)[N][NR]) {
+  if constexpr (N == 1) {
+    const double w = W(0, 0);
+    const double iw = 1.0 / w;
+    NOC_UNROLL for (int j = 0; j < NR; ++j) Y[0][j] *= iw;
+    return w > 0.0;
+  } else {
+    double D[N], iD[N];
+    double Lm[N][N];
+    bool pd = true;
+    NOC_UNROLL for (int j = 0; j < N; ++j) {
+      double dj = W(j, j);
+      NOC_UNROLL for (int t = 0; t < j; ++t) dj -= Lm[j][t] * Lm[j][t] * D[t];
+      D[j] = dj;
+      iD[j] = 1.0 / dj;
+      pd = pd && (dj > 0.0);
+      NOC_UNROLL for (int i = j + 1; i < N; ++i) {
+        double s = W(i, j);
+        NOC_UNROLL for (int t = 0; t < j; ++t) s -= Lm[i][t] * Lm[j][t] * D[t];
+        Lm[i][j] = s * iD[j];
+      }
+    }
+    // L z = y
+    NOC_UNROLL for (int i = 0; i < N; ++i)
+      NOC_UNROLL for (int t = 0; t < i; ++t)
+        NOC_UNROLL for (int j = 0; j < NR; ++j) Y[i][j] -= Lm[i][t] * Y[t][j];
+    NOC_UNROLL for (int i = 0; i < N; ++i) NOC_UNROLL for (int j = 0; j < NR; ++j) Y[i][j] *= iD[i];
+    // L' x = z
+    NOC_UNROLL for (int i = N - 1; i >= 0; --i)
+      NOC_UNROLL for (int t = i + 1; t < N; ++t)
+        NOC_UNROLL for (int j = 0; j < NR; ++j) Y[i][j] -= Lm[t][i] * Y[t][j];
+    return pd;
+  }
+}
+
+// Gaussian elimination with partial pivoting (row swaps as selects, so everything stays in
+// VGPRs).  X (N x N) is destroyed; Y (N x NR) becomes X^{-1} Y.
+template <int N, int NR>
+NOC_DEV void lu_pp_solve(double (&X)[N][N], double (&Y)[N][NR]) {
+  NOC_UNROLL for (int k = 0; k < N; ++k) {
+    if constexpr (N > 1) {
+      int piv = k;
+      double best = fabs(X[k][k]);
+      NOC_UNROLL for (int i = k + 1; i < N; ++i) {
+        const double a = fabs(X[i][k]);
+        const bool better = a > best;
+        best = better ? a : best;
+        piv = better ? i : piv;
+      }
+      NOC_UNROLL for (int i = k + 1; i < N; ++i) {
+        const bool sw = (piv == i);
+        NOC_UNROLL for (int j = k; j < N; ++j) {
+          const double a = X[k][j], b = X[i][j];
+          X[k][j] = sw ? b : a;
+          X[i][j] = sw ? a : b;
+        }
+        NOC_UNROLL for (int j = 0; j < NR; ++j) {
+          const double a = Y[k][j], b = Y[i][j];
+          Y[k][j] = sw ? b : a;
+          Y[i][j] = sw ? a : b;
+        }
+      }
+    }
+    const double inv = 1.0 / X[k][k];
+    X[k][k] = inv;
+    NOC_UNROLL for (int i = k + 1; i < N; ++i) {
+      const double lik = X[i][k] * inv;
+      NOC_UNROLL for (int j = k + 1; j < N; ++j) X[i][j] -= lik * X[k][j];
+      NOC_UNROLL for (int j = 0; j < NR; ++j) Y[i][j] -= lik * Y[k][j];
+    }
+  }
+  NOC_UNROLL for (int k = N - 1; k >= 0; --k) {
+    NOC_UNROLL for (int j = 0; j < NR; ++j) {
+      double s = Y[k][j];
+      NOC_UNROLL for (int t = k + 1; t < N; ++t) s -= X[k][t] * Y[t][j];
+      Y[k][j] = s * X[k][k];
+    }
+  }
+}
+
+}  // namespace noc

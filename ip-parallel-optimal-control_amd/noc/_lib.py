@@ -1,0 +1,117 @@
+"""ctypes binding of libnoc_hip.so (the C-ABI declared in include/noc_hip.h).
+
+The product path has no CPU fallback: if the shared library is missing or no GPU is visible,
+every compute entry point raises.  Building: `make -C ip-parallel-optimal-control_amd -j8`
+(or `python -c "import __graft_entry__ as g; g.build()"` from the repo root).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NOC_HIP_LIB", os.path.join(_HERE, "_lib", "libnoc_hip.so"))
+
+_dp = ctypes.c_void_p  # device pointers are passed as opaque addresses
+_i = ctypes.c_int
+
+# name -> (restype, argtypes); mirrors include/noc_hip.h exactly (tests check every symbol)
+SIGNATURES = {
+    "noc_abi_version": (_i, []),
+    "noc_last_error": (ctypes.c_char_p, []),
+    "noc_kkt_supported": (_i, [_i, _i]),
+    "noc_kkt_default_lanes": (_i, [_i, _i, _i]),
+    "noc_kkt_solve": (_i, [_i] * 5 + [_dp] * 13 + [_dp] * 8 + [_dp]),
+    "noc_par_bwd_pass": (_i, [_i] * 5 + [_dp] * 12 + [_dp] * 6 + [_dp]),
+    "noc_par_fwd_pass": (_i, [_i] * 5 + [_dp] * 7 + [_dp] * 2 + [_dp]),
+}
+
+# --- structs of include/noc_hip.h --------------------------------------------------------------
+FAMILY_PENDULUM, FAMILY_CARTPOLE, FAMILY_LINEAR = 1, 2, 3
+PHASE_ROLLOUT, PHASE_LINEARIZE, PHASE_SOLVE, PHASE_DONE = 0, 1, 2, 3
+MODE_PAR, MODE_SEQ = 0, 1
+TERMINAL_FINAL_COST, TERMINAL_STAGE0 = 0, 1
+
+
+class NocFamily(ctypes.Structure):
+    _fields_ = [("kind", _i), ("nx", _i), ("nu", _i), ("wrap_index", _i),
+                ("dt", ctypes.c_double), ("u_bound", ctypes.c_double),
+                ("goal", ctypes.c_double * 8), ("wx", ctypes.c_double * 8),
+                ("wu", ctypes.c_double * 4), ("wf", ctypes.c_double * 8),
+                ("A", ctypes.c_double * 64), ("B", ctypes.c_double * 32)]
+
+
+WS_DOUBLE_FIELDS = ["x", "u", "x0", "A", "B", "Q", "R", "M", "r", "P", "cx", "cu", "lc", "lam",
+                    "dx", "du", "pred", "K", "d"]
+WS_INT_FIELDS = ["feasible", "phase", "kkt_active", "it", "inner", "total_it", "kkt_solves"]
+WS_STATE_FIELDS = ["bp", "rp", "rinc", "cost", "hu", "gnorm", "reg"]
+
+
+class NocIpmWs(ctypes.Structure):
+    _fields_ = ([("Bt", _i), ("N", _i)] + [(f, _dp) for f in WS_DOUBLE_FIELDS]
+                + [(f, _dp) for f in WS_INT_FIELDS] + [(f, _dp) for f in WS_STATE_FIELDS])
+
+
+_fp = ctypes.POINTER(NocFamily)
+_wp = ctypes.POINTER(NocIpmWs)
+SIGNATURES.update({
+    "noc_family_supported": (_i, [_fp]),
+    "noc_ipm_init": (_i, [_wp, ctypes.c_double, _dp]),
+    "noc_ipm_prepare": (_i, [_fp, _wp, _i, _i, _dp]),
+    "noc_ipm_trial": (_i, [_fp, _wp, _i, _dp]),
+    "noc_ipm_step": (_i, [_fp, _wp, _i, _i, _i, _dp]),
+})
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class NocError(RuntimeError):
+    pass
+
+
+def load(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load (once) and type the shared library.  Raises NocError if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise NocError(f"libnoc_hip.so not found at {p}; build it with "
+                       f"`make -C ip-parallel-optimal-control_amd -j8`")
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.noc_abi_version() != 1:
+        raise NocError("libnoc_hip.so ABI version mismatch")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().noc_last_error().decode(errors="replace")
+        raise NocError(f"{what} failed (rc={rc}): {msg}")
+
+
+def ptr(t) -> Optional[int]:
+    """Device address of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def require_device(t, name: str):
+    import torch
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise NocError(f"{name}: expected a CUDA (HIP) torch tensor; the MI355X path has no "
+                       f"CPU fallback")
+    return t
+
+
+def stream_handle(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,96 @@
+"""Batched interior-point engine: device workspace + host loop over libnoc_hip.so.
+
+The reference runs one trajectory per call, with its whole solve as nested lax.while_loops
+(noc/par_interior_point_newton.py:127-254).  Here B trajectories run at once; every trajectory
+carries its own phase / counters / barrier parameter on the device, so each one follows exactly
+its own reference control flow (jax.vmap semantics), while the host only launches one fused
+iteration (rollout | linearise | costate | assemble | KKT scan | trial) at a time and polls a
+single "any trajectory not done" flag every `poll_every` iterations.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+class BatchedIPM:
+    def __init__(self, family, N: int, batch: int, device="cuda", lanes: int = 0):
+        if not torch.cuda.is_available():
+            raise _lib.NocError("no HIP device visible: the MI355X path has no CPU fallback")
+        self.family = family
+        self.fam_c = family.to_c()
+        self.N, self.Bt = int(N), int(batch)
+        self.nx, self.nu = family.nx, family.nu
+        self.device = torch.device(device)
+        self.lanes = lanes
+        lib = _lib.load()
+        if not lib.noc_family_supported(ctypes.byref(self.fam_c)):
+            raise _lib.NocError(f"unsupported family kind={family.kind} nx={family.nx} nu={family.nu}")
+        Bt, N, nx, nu = self.Bt, self.N, self.nx, self.nu
+        f64 = dict(device=self.device, dtype=torch.float64)
+        i32 = dict(device=self.device, dtype=torch.int32)
+        shapes = dict(x=(Bt, N + 1, nx), u=(Bt, N, nu), x0=(Bt, nx), A=(Bt, N, nx, nx),
+                      B=(Bt, N, nx, nu), Q=(Bt, N, nx, nx), R=(Bt, N, nu, nu), M=(Bt, N, nx, nu),
+                      r=(Bt, N, nu), P=(Bt, nx, nx), cx=(Bt, N, nx), cu=(Bt, N, nu), lc=(Bt, N),
+                      lam=(Bt, N + 1, nx), dx=(Bt, N + 1, nx), du=(Bt, N, nu), pred=(Bt,),
+                      K=(Bt, N, nu, nx), d=(Bt, N, nu))
+        self.t = {k: torch.zeros(s, **f64) for k, s in shapes.items()}
+        for k in _lib.WS_INT_FIELDS:
+            self.t[k] = torch.zeros(Bt, **i32)
+        for k in _lib.WS_STATE_FIELDS:
+            self.t[k] = torch.zeros(Bt, **f64)
+        ws = _lib.NocIpmWs()
+        ws.Bt, ws.N = Bt, N
+        for k in _lib.WS_DOUBLE_FIELDS + _lib.WS_INT_FIELDS + _lib.WS_STATE_FIELDS:
+            setattr(ws, k, self.t[k].data_ptr())
+        self.ws = ws
+        self._lib = lib
+
+    # -------------------------------------------------------------------------------------------
+    def load(self, controls, initial_state):
+        u = torch.as_tensor(np.asarray(controls, dtype=np.float64)).reshape(self.Bt, self.N, self.nu)
+        x0 = torch.as_tensor(np.asarray(initial_state, dtype=np.float64)).reshape(self.Bt, self.nx)
+        self.t["u"].copy_(u)
+        self.t["x0"].copy_(x0)
+
+    def _stream(self):
+        return _lib.stream_handle(self.device)
+
+    def init(self, bp0: float = 0.1):
+        _lib.check(self._lib.noc_ipm_init(ctypes.byref(self.ws), float(bp0), self._stream()),
+                   "noc_ipm_init")
+
+    def prepare(self, mode: int, terminal: int):
+        _lib.check(self._lib.noc_ipm_prepare(ctypes.byref(self.fam_c), ctypes.byref(self.ws), mode,
+                                             terminal, self._stream()), "noc_ipm_prepare")
+
+    def step(self, mode: int, terminal: int):
+        _lib.check(self._lib.noc_ipm_step(ctypes.byref(self.fam_c), ctypes.byref(self.ws), mode,
+                                          terminal, self.lanes, self._stream()), "noc_ipm_step")
+
+    def all_done(self) -> bool:
+        return not bool(torch.any(self.t["phase"] != _lib.PHASE_DONE).item())
+
+    def solve(self, mode: int = _lib.MODE_PAR, terminal: int = _lib.TERMINAL_FINAL_COST,
+              bp0: float = 0.1, poll_every: int = 8, max_steps: Optional[int] = None):
+        """Run the barrier schedule to completion for every trajectory.  Returns the number of
+        device iterations (= KKT solves of the slowest trajectory)."""
+        self.init(bp0)
+        steps = 0
+        limit = max_steps if max_steps is not None else 10 ** 9
+        while steps < limit:
+            for _ in range(poll_every):
+                self.step(mode, terminal)
+                steps += 1
+            if self.all_done():
+                break
+        return steps
+
+    # -------------------------------------------------------------------------------------------
+    def result(self):
+        return (self.t["u"].clone(), self.t["total_it"].clone(), self.t["kkt_solves"].clone())

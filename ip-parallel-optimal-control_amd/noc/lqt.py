@@ -1,0 +1,195 @@
+"""Batched LQ (KKT) solves on the MI355X -- the drop-in for `paroc` as used by the reference.
+
+Reference call sites replaced:
+  * noc/par_interior_point_newton.py:119-123 (par_Newton: noc_to_lqt -> par_bwd_pass -> par_fwd_pass)
+  * examples/linear_mpc_parallel.py:64-75 (LQT(...), par_bwd_pass(lqt), par_fwd_pass(lqt, x0, Kx, d))
+
+Two levels of API:
+  * `kkt_solve(...)`: the canonical stage form used by the interior-point Newton step
+    (include/noc_hip.h), batched over a leading trajectory axis; one fused HIP launch.
+  * `LQT` + `par_bwd_pass` / `par_fwd_pass` / `seq_bwd_pass` / `seq_fwd_pass`: paroc's 13-field
+    tracking form (field order from LM:64 and P:69-83), batched or not.  The tracking form is
+    converted to the canonical form on the device (a few batched einsums), then the same HIP
+    kernels run.  The "seq" names are kept for API compatibility and run the same kernels.
+
+All tensors are torch fp64 CUDA tensors; calls are asynchronous on the current stream.
+"""
+from __future__ import annotations
+
+from typing import NamedTuple, Optional
+
+import torch
+
+from . import _lib
+
+
+class KKTResult(NamedTuple):
+    dx: torch.Tensor          # (Bt, N+1, nx)
+    du: torch.Tensor          # (Bt, N, nu)
+    pred: torch.Tensor        # (Bt,)  sum of dV (noc/seq_interior_point_newton.py:63,75)
+    feasible: torch.Tensor    # (Bt,) int32, all Quu > 0 (S:52-53)
+    K: torch.Tensor           # (Bt, N, nu, nx)
+    d: torch.Tensor           # (Bt, N, nu)
+    S: Optional[torch.Tensor]  # (Bt, N+1, nx, nx) or None
+    v: Optional[torch.Tensor]  # (Bt, N+1, nx) or None
+
+
+def _c(t, name):
+    if t is None:
+        return None
+    _lib.require_device(t, name)
+    if t.dtype != torch.float64:
+        raise _lib.NocError(f"{name}: expected float64, got {t.dtype}")
+    return t.contiguous()
+
+
+def _batched(*ts):
+    """Accept unbatched (N, ...) inputs like the reference; returns (squeeze flag, tensors)."""
+    A = ts[0]
+    if A.dim() == 3:
+        return True, [None if t is None else t.unsqueeze(0) for t in ts]
+    return False, list(ts)
+
+
+def kkt_solve(A, B, Q, R, M, r, P, reg=None, x0=None, q=None, c=None, p=None, active=None,
+              lanes: int = 0, want_value: bool = False, out: Optional[KKTResult] = None,
+              ) -> KKTResult:
+    """Batched fused KKT solve (bwd + fwd).  Shapes (leading batch Bt optional):
+    A (Bt,N,nx,nx) B (Bt,N,nx,nu) Q (Bt,N,nx,nx) R (Bt,N,nu,nu) M (Bt,N,nx,nu) r (Bt,N,nu)
+    P (Bt,nx,nx) reg (Bt,) x0/p (Bt,nx) q/c (Bt,N,nx) active (Bt,) int32."""
+    squeeze, (A, B, Q, R, M, r, P, x0, q, c, p) = _batched(A, B, Q, R, M, r, P, x0, q, c, p)
+    if squeeze and reg is not None and reg.dim() == 0:
+        reg = reg.reshape(1)
+    A, B, Q, R, M, r, P = (_c(t, n) for t, n in zip((A, B, Q, R, M, r, P), "A B Q R M r P".split()))
+    x0, q, c, p, reg = _c(x0, "x0"), _c(q, "q"), _c(c, "c"), _c(p, "p"), _c(reg, "reg")
+    Bt, N, nx, _ = A.shape
+    nu = B.shape[-1]
+    dev = A.device
+    if active is not None:
+        active = active.to(device=dev, dtype=torch.int32).contiguous()
+    if out is None:
+        f64 = dict(device=dev, dtype=torch.float64)
+        out = KKTResult(
+            torch.empty(Bt, N + 1, nx, **f64), torch.empty(Bt, N, nu, **f64),
+            torch.empty(Bt, **f64), torch.empty(Bt, device=dev, dtype=torch.int32),
+            torch.empty(Bt, N, nu, nx, **f64), torch.empty(Bt, N, nu, **f64),
+            torch.empty(Bt, N + 1, nx, nx, **f64) if want_value else None,
+            torch.empty(Bt, N + 1, nx, **f64) if want_value else None)
+    lib = _lib.load()
+    rc = lib.noc_kkt_solve(nx, nu, N, Bt, lanes, *(_lib.ptr(t) for t in (
+        A, B, Q, R, M, r, q, c, P, p, x0, reg, active,
+        out.dx, out.du, out.pred, out.feasible, out.K, out.d, out.S, out.v)),
+        _lib.stream_handle(dev))
+    _lib.check(rc, "noc_kkt_solve")
+    if squeeze:
+        out = KKTResult(*(None if t is None else t[0] for t in out))
+    return out
+
+
+def bwd_pass(A, B, Q, R, M, r, P, reg=None, q=None, c=None, p=None, active=None, lanes=0):
+    """Backward pass only -> (K, d, S, v, pred, feasible) (paroc.par_bwd_pass semantics)."""
+    squeeze, (A, B, Q, R, M, r, P, q, c, p) = _batched(A, B, Q, R, M, r, P, q, c, p)
+    A, B, Q, R, M, r, P = (_c(t, n) for t, n in zip((A, B, Q, R, M, r, P), "A B Q R M r P".split()))
+    q, c, p, reg = _c(q, "q"), _c(c, "c"), _c(p, "p"), _c(reg, "reg")
+    Bt, N, nx, _ = A.shape
+    nu = B.shape[-1]
+    f64 = dict(device=A.device, dtype=torch.float64)
+    K = torch.empty(Bt, N, nu, nx, **f64)
+    d = torch.empty(Bt, N, nu, **f64)
+    S = torch.empty(Bt, N + 1, nx, nx, **f64)
+    v = torch.empty(Bt, N + 1, nx, **f64)
+    pred = torch.empty(Bt, **f64)
+    feas = torch.empty(Bt, device=A.device, dtype=torch.int32)
+    if active is not None:
+        active = active.to(device=A.device, dtype=torch.int32).contiguous()
+    rc = _lib.load().noc_par_bwd_pass(nx, nu, N, Bt, lanes, *(_lib.ptr(t) for t in (
+        A, B, Q, R, M, r, q, c, P, p, reg, active, K, d, S, v, pred, feas)),
+        _lib.stream_handle(A.device))
+    _lib.check(rc, "noc_par_bwd_pass")
+    res = (K, d, S, v, pred, feas)
+    return tuple(t[0] for t in res) if squeeze else res
+
+
+def fwd_pass(A, B, K, d, x0=None, c=None, active=None, lanes=0):
+    """Forward pass only -> (du, dx) (paroc.par_fwd_pass semantics)."""
+    squeeze, (A, B, K, d, x0, c) = _batched(A, B, K, d, x0, c)
+    A, B, K, d = _c(A, "A"), _c(B, "B"), _c(K, "K"), _c(d, "d")
+    x0, c = _c(x0, "x0"), _c(c, "c")
+    Bt, N, nx, _ = A.shape
+    nu = B.shape[-1]
+    f64 = dict(device=A.device, dtype=torch.float64)
+    du = torch.empty(Bt, N, nu, **f64)
+    dx = torch.empty(Bt, N + 1, nx, **f64)
+    if active is not None:
+        active = active.to(device=A.device, dtype=torch.int32).contiguous()
+    rc = _lib.load().noc_par_fwd_pass(nx, nu, N, Bt, lanes, *(_lib.ptr(t) for t in (
+        A, B, c, x0, K, d, active, du, dx)), _lib.stream_handle(A.device))
+    _lib.check(rc, "noc_par_fwd_pass")
+    return (du[0], dx[0]) if squeeze else (du, dx)
+
+
+# ------------------------------------------------------------------------------------------------
+# paroc-compatible tracking-form LQT (field order: LM:64, P:69-83)
+# ------------------------------------------------------------------------------------------------
+class LQT(NamedTuple):
+    """paroc.lqt_problem.LQT: dynamics x+ = F x + L u + c; stage cost
+    1/2 (Hx - r)'X(Hx - r) + 1/2 (Zu - s)'U(Zu - s) + (Hx - r)'M(Zu - s); terminal cost
+    1/2 (HT x - rT)'XT(HT x - rT).  (Convention consistent with noc_to_lqt, P:62-66.)"""
+    F: torch.Tensor
+    L: torch.Tensor
+    c: torch.Tensor
+    XT: torch.Tensor
+    HT: torch.Tensor
+    rT: torch.Tensor
+    X: torch.Tensor
+    H: torch.Tensor
+    r: torch.Tensor
+    U: torch.Tensor
+    Z: torch.Tensor
+    s: torch.Tensor
+    M: torch.Tensor
+
+
+def lqt_to_canonical(lqt: LQT):
+    """Expand the tracking form into (A, B, Q, R, M, r, q, c, P, p) (batched einsums)."""
+    H, Z, X, U, Mt = lqt.H, lqt.Z, lqt.X, lqt.U, lqt.M
+    t = lambda x: x.transpose(-1, -2)
+    Q = t(H) @ X @ H
+    R = t(Z) @ U @ Z
+    M = t(H) @ Mt @ Z
+    rr, ss = lqt.r.unsqueeze(-1), lqt.s.unsqueeze(-1)
+    q = -(t(H) @ (X @ rr + Mt @ ss)).squeeze(-1)
+    r = -(t(Z) @ (U @ ss + t(Mt) @ rr)).squeeze(-1)
+    P = t(lqt.HT) @ lqt.XT @ lqt.HT
+    p = -(t(lqt.HT) @ (lqt.XT @ lqt.rT.unsqueeze(-1))).squeeze(-1)
+    return lqt.F, lqt.L, Q, R, M, r, q, lqt.c, P, p
+
+
+def _aff(t):
+    return None if t is None or not bool(torch.any(t != 0)) else t.contiguous()
+
+
+def par_bwd_pass(lqt: LQT, lanes: int = 0):
+    """paroc.par_bwd_pass(lqt) -> (Kx, d, S, v, pred_reduction, feasible); du = Kx dx + d."""
+    A, B, Q, R, M, r, q, c, P, p = lqt_to_canonical(lqt)
+    K, d, S, v, pred, feas = bwd_pass(A.contiguous(), B.contiguous(), Q.contiguous(),
+                                      R.contiguous(), M.contiguous(), r.contiguous(), P.contiguous(),
+                                      q=_aff(q), c=_aff(c), p=_aff(p), lanes=lanes)
+    return K, d, S, v, pred, feas.bool()
+
+
+def par_fwd_pass(lqt: LQT, x0, Kx, d, lanes: int = 0):
+    """paroc.par_fwd_pass(lqt, x0, Kx, d) -> (u, x)."""
+    return fwd_pass(lqt.F.contiguous(), lqt.L.contiguous(), Kx, d, x0=x0.contiguous(),
+                    c=_aff(lqt.c), lanes=lanes)
+
+
+def seq_bwd_pass(lqt: LQT):
+    """paroc.seq_bwd_pass(lqt) -> (Kx, d, S, v) (LM:74).  Same solution; same HIP kernels."""
+    K, d, S, v, _, _ = par_bwd_pass(lqt)
+    return K, d, S, v
+
+
+def seq_fwd_pass(lqt: LQT, x0, Kx, d):
+    """paroc.seq_fwd_pass(lqt, x0, Kx, d) -> (u, x) (LM:75)."""
+    return par_fwd_pass(lqt, x0, Kx, d)

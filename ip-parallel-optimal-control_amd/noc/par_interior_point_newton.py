@@ -1,0 +1,49 @@
+"""Parallel-in-time interior-point solver -- drop-in for noc/par_interior_point_newton.py.
+
+`par_interior_point_optimal_control(ocp, controls, initial_state) -> (controls*, iterations)`
+keeps the reference signature (P:228-254).  Differences, all additive:
+  * inputs may carry a leading batch axis (controls (B, N, nu), initial_state (B, nx)); the
+    result is then batched too -- each trajectory follows its own reference control flow;
+  * the whole loop runs on the MI355X (libnoc_hip.so); `ocp.family` must be a registered family
+    (noc.problems) because device code cannot call Python callables;
+  * `terminal`: "final_cost" (default; terminal Hessian = hessian(final_cost), identical to the
+    reference's seq path S:66) or "stage0" (the reference par path's XT = Q[0], P:73).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .ipm import BatchedIPM
+from .optimal_control_problem import OCP
+
+_TERMINAL = {"final_cost": _lib.TERMINAL_FINAL_COST, "stage0": _lib.TERMINAL_STAGE0}
+
+
+def _run(ocp: OCP, controls, initial_state, mode, terminal="final_cost", lanes=0,
+         device="cuda", return_info=False):
+    if ocp.family is None:
+        raise _lib.NocError("OCP has no registered device family (use noc.problems.*): the HIP "
+                            "kernels cannot evaluate Python callables")
+    u = np.asarray(controls, dtype=np.float64)
+    x0 = np.asarray(initial_state, dtype=np.float64)
+    single = u.ndim == 2
+    if single:
+        u, x0 = u[None], x0[None]
+    Bt, N, _ = u.shape
+    eng = BatchedIPM(ocp.family, N, Bt, device=device, lanes=lanes)
+    eng.load(u, x0)
+    steps = eng.solve(mode=mode, terminal=_TERMINAL[terminal])
+    U, iters, solves = eng.result()
+    U, iters, solves = U.cpu().numpy(), iters.cpu().numpy(), solves.cpu().numpy()
+    if single:
+        U, iters, solves = U[0], int(iters[0]), int(solves[0])
+    if return_info:
+        return U, iters, dict(kkt_solves=solves, device_steps=steps)
+    return U, iters
+
+
+def par_interior_point_optimal_control(ocp: OCP, controls, initial_state, terminal="final_cost",
+                                       lanes: int = 0, device="cuda", return_info=False):
+    """P:228-254: barrier 0.1 / 5^k while > 1e-4; Newton with retry loop; returns (u*, iters)."""
+    return _run(ocp, controls, initial_state, _lib.MODE_PAR, terminal, lanes, device, return_info)

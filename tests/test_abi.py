@@ -1,0 +1,100 @@
+"""CPU-side checks of the C-ABI: libnoc_hip.so loads, exports every symbol include/noc_hip.h
+declares, the ctypes mirror matches the header, and argument validation fails loudly (no compute
+calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "noc_hip.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(noc_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = header_functions()
+    for f in ["noc_kkt_solve", "noc_par_bwd_pass", "noc_par_fwd_pass", "noc_ipm_step",
+              "noc_ipm_prepare", "noc_ipm_trial", "noc_ipm_init", "noc_abi_version"]:
+        assert f in fns
+
+
+def test_library_exports_every_header_symbol():
+    from noc import _lib
+    lib = _lib.load()
+    for f in header_functions():
+        assert hasattr(lib, f), f
+        assert f in _lib.SIGNATURES, f"ctypes mirror lacks {f}"
+    assert lib.noc_abi_version() == 1
+
+
+def test_supported_shapes_and_lanes():
+    from noc import _lib
+    lib = _lib.load()
+    assert lib.noc_kkt_supported(4, 1) == 1
+    assert lib.noc_kkt_supported(2, 1) == 1
+    assert lib.noc_kkt_supported(8, 4) == 1
+    assert lib.noc_kkt_supported(3, 1) == 0
+    assert lib.noc_kkt_default_lanes(4, 1, 200) in (8, 16, 32, 64)
+
+
+def test_argument_errors_are_reported_not_launched():
+    from noc import _lib
+    lib = _lib.load()
+    rc = lib.noc_kkt_solve(3, 1, 10, 4, 0, *([None] * 21), None)
+    assert rc < 0 and b"unsupported" in lib.noc_last_error()
+    rc = lib.noc_kkt_solve(4, 1, 10, 4, 0, *([None] * 21), None)
+    assert rc < 0 and b"NULL" in lib.noc_last_error()
+    rc = lib.noc_kkt_solve(4, 1, 0, 4, 0, *([None] * 21), None)
+    assert rc < 0 and b"horizon" in lib.noc_last_error()
+    rc = lib.noc_kkt_solve(4, 1, 10, 4, 48, *([None] * 21), None)
+    assert rc < 0 and b"lanes" in lib.noc_last_error()
+    # misaligned pointer is rejected before any launch
+    rc = lib.noc_kkt_solve(4, 1, 10, 4, 0, 8, *([16] * 20), None)
+    assert rc < 0 and b"aligned" in lib.noc_last_error()
+
+
+def test_workspace_struct_layout_matches_header():
+    from noc import _lib
+    text = open(HEADER).read()
+    body = re.search(r"typedef struct noc_ipm_ws \{(.*?)\} noc_ipm_ws;", text, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = re.findall(r"\*?\s*\*?(\w+)\s*[,;]", body.replace("*", " "))
+    names = [n for n in names if n not in ("int", "double")]
+    assert names == [f for f, _ in _lib.NocIpmWs._fields_]
+    assert ctypes.sizeof(_lib.NocFamily) == 4 * 4 + 8 * 2 + 8 * (8 + 8 + 4 + 8 + 64 + 32)
+
+
+def test_family_validation_without_gpu():
+    from noc import _lib, problems
+    lib = _lib.load()
+    for ocp in (problems.pendulum(0.02), problems.cartpole(0.005), problems.double_integrators(4, 0.001),
+                problems.double_integrators(1, 0.1)):
+        fam = ocp.family.to_c()
+        assert lib.noc_family_supported(ctypes.byref(fam)) == 1
+    bad = problems.pendulum(0.02).family
+    bad.nx = 3
+    assert lib.noc_family_supported(ctypes.byref(bad.to_c())) == 0
+
+
+def test_product_path_fails_loudly_without_gpu():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from noc import _lib, problems
+    from noc.par_interior_point_newton import par_interior_point_optimal_control
+    import numpy as np
+    with pytest.raises(_lib.NocError):
+        par_interior_point_optimal_control(problems.pendulum(0.02), np.zeros((50, 1)), np.zeros(2))
+    from noc import lqt
+    with pytest.raises(_lib.NocError):
+        z = torch.zeros(1, 5, 4, 4, dtype=torch.float64)
+        lqt.kkt_solve(z, torch.zeros(1, 5, 4, 1, dtype=torch.float64), z,
+                      torch.ones(1, 5, 1, 1, dtype=torch.float64),
+                      torch.zeros(1, 5, 4, 1, dtype=torch.float64),
+                      torch.zeros(1, 5, 1, dtype=torch.float64), torch.eye(4, dtype=torch.float64)[None])

@@ -1,0 +1,155 @@
+"""GPU parity of the device linearisation and of the whole batched interior-point solve against
+the oracle (oracle/noc_oracle.py restating P:127-254 and S:108-202; derivatives by torch.func
+autodiff, oracle/problems.py).
+
+Tolerances (fp64, stated): LQ blocks 1e-10 relative; full solves: identical outer-iteration and
+KKT-solve counts, final cost relative 1e-8, controls 1e-6 absolute (the step sequence is the same;
+only rounding differs).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def _oracle_problem(name, N):
+    from oracle import problems as PR, noc_oracle as O
+    if name == "pendulum":
+        return O.NumpyProblem(PR.pendulum_ocp(1.0 / N))
+    if name == "cartpole":
+        return O.NumpyProblem(PR.cartpole_ocp(1.0 / N))
+    raise ValueError(name)
+
+
+@pytest.mark.parametrize("name,N", [("pendulum", 50), ("cartpole", 40)])
+def test_device_linearisation_matches_autodiff_oracle(name, N):
+    from noc.problems import make_bench_blocks
+    from oracle import noc_oracle as O
+    blk = make_bench_blocks(name, N=N, batch=3, seed=5)
+    torch.cuda.synchronize()
+    prob = _oracle_problem(name, N)
+    X = blk["x"].cpu().numpy()
+    U = blk["u"].cpu().numpy()
+    eng = blk["engine"]
+    for b in range(3):
+        ref_x = O.rollout(prob.dynamics, U[b], X[b, 0])
+        assert _rel(X[b], ref_x) < 1e-12
+        L = O.linearize(prob, X[b], U[b], 0.1)
+        for k in ["A", "B", "Q", "R", "M", "r", "P"]:
+            assert _rel(blk[k][b].cpu().numpy(), L[k]) < 1e-10, (k, _rel(blk[k][b].cpu(), L[k]))
+        cost = prob.total_cost(X[b], U[b], 0.1)
+        assert abs(eng.t["cost"][b].item() - cost) <= 1e-12 * abs(cost)
+        assert abs(eng.t["hu"][b].item() - np.max(np.abs(L["r"]))) <= 1e-12
+        assert abs(eng.t["gnorm"][b].item() - np.linalg.norm(L["cu"])) <= 1e-12 * np.linalg.norm(L["cu"])
+
+
+def test_pendulum_par_solve_matches_oracle():
+    """BASELINE config c1 (pendulum N=50, B=1): same iterations / KKT solves as the oracle."""
+    from noc import problems
+    from noc.par_interior_point_newton import par_interior_point_optimal_control
+    from oracle import noc_oracle as O
+    N = 50
+    ocp = problems.pendulum(1.0 / N)
+    u0 = 0.1 * np.random.default_rng(1).normal(size=(N, 1))
+    x0 = np.array([0.1, -0.1])
+    U, it, info = par_interior_point_optimal_control(ocp, u0, x0, return_info=True)
+    prob = _oracle_problem("pendulum", N)
+    Ur, itr, solves_r = O.par_interior_point_optimal_control(prob, u0, x0)
+    assert it == itr == 70
+    assert info["kkt_solves"] == solves_r == 87
+    c = prob.total_cost(O.rollout(prob.dynamics, U, x0), U, 0.0)
+    cr = prob.total_cost(O.rollout(prob.dynamics, Ur, x0), Ur, 0.0)
+    assert abs(c - cr) <= 1e-8 * abs(cr)
+    assert np.max(np.abs(U - Ur)) < 1e-6
+
+
+def test_pendulum_seq_solve_matches_oracle():
+    from noc import problems
+    from noc.seq_interior_point_newton import seq_interior_point_optimal_control
+    from oracle import noc_oracle as O
+    N = 50
+    ocp = problems.pendulum(1.0 / N)
+    u0 = 0.1 * np.random.default_rng(1).normal(size=(N, 1))
+    x0 = np.array([0.1, -0.1])
+    U, it = seq_interior_point_optimal_control(ocp, u0, x0)
+    prob = _oracle_problem("pendulum", N)
+    Ur, itr = O.seq_interior_point_optimal_control(prob, u0, x0)
+    assert it == itr == 79
+    assert np.max(np.abs(U - Ur)) < 1e-6
+
+
+def test_batched_solve_equals_individual_oracle_runs():
+    """vmap semantics: every trajectory of a batch follows its own reference control flow."""
+    from noc import problems
+    from noc.par_interior_point_newton import par_interior_point_optimal_control
+    from oracle import noc_oracle as O
+    N, Bt = 30, 4
+    ocp = problems.pendulum(1.0 / N)
+    x0, u0 = problems.initial_conditions("pendulum", N, Bt, seed=9)
+    U, its, info = par_interior_point_optimal_control(ocp, u0, x0, return_info=True)
+    prob = _oracle_problem("pendulum", N)
+    for b in range(Bt):
+        Ur, itr, sr = O.par_interior_point_optimal_control(prob, u0[b], x0[b])
+        assert its[b] == itr and info["kkt_solves"][b] == sr
+        assert np.max(np.abs(U[b] - Ur)) < 1e-6
+
+
+def test_cartpole_par_solve_matches_oracle():
+    from noc import problems
+    from noc.par_interior_point_newton import par_interior_point_optimal_control
+    from oracle import noc_oracle as O
+    N = 40
+    ocp = problems.cartpole(1.0 / N)
+    x0, u0 = problems.initial_conditions("cartpole", N, 1, seed=3)
+    U, it, info = par_interior_point_optimal_control(ocp, u0[0], x0[0], return_info=True)
+    prob = _oracle_problem("cartpole", N)
+    Ur, itr, sr = O.par_interior_point_optimal_control(prob, u0[0], x0[0])
+    assert it == itr and info["kkt_solves"] == sr
+    c = prob.total_cost(O.rollout(prob.dynamics, U, x0[0]), U, 0.0)
+    cr = prob.total_cost(O.rollout(prob.dynamics, Ur, x0[0]), Ur, 0.0)
+    assert abs(c - cr) <= 1e-8 * abs(cr)
+
+
+def test_stage0_terminal_option_runs():
+    """The reference par path's XT = Q[0] quirk (P:73) is reproducible on request."""
+    from noc import problems
+    from noc.par_interior_point_newton import par_interior_point_optimal_control
+    from oracle import noc_oracle as O
+    N = 30
+    ocp = problems.pendulum(1.0 / N)
+    u0 = 0.1 * np.random.default_rng(1).normal(size=(N, 1))
+    x0 = np.array([0.1, -0.1])
+    U, it = par_interior_point_optimal_control(ocp, u0, x0, terminal="stage0")
+    prob = _oracle_problem("pendulum", N)
+    Ur, itr, _ = O.par_interior_point_optimal_control(prob, u0, x0, terminal="stage0")
+    assert it == itr
+    assert np.max(np.abs(U - Ur)) < 1e-6
+
+
+def test_linear_demo_known_answer():
+    """examples/linear_demo_cuda.py (LD:123-166): unconstrained LQR, one exact Newton step solves
+    it; compare with the dense KKT solution of the same LQ problem."""
+    from noc import problems
+    from noc.par_interior_point_newton import par_interior_point_optimal_control
+    from oracle import noc_oracle as O
+    N = 40
+    ocp = problems.double_integrators(1, 0.1)
+    x0 = np.array([2.0, 1.0])
+    u0 = np.zeros((N, 1))
+    U, it = par_interior_point_optimal_control(ocp, u0, x0)
+    fam = ocp.family
+    A = np.repeat(fam.A[None], N, 0)
+    B = np.repeat(fam.B[None], N, 0)
+    Q = np.repeat(np.diag(fam.wx)[None], N, 0)
+    R = np.repeat(np.diag(fam.wu)[None], N, 0)
+    M = np.zeros((N, 2, 1))
+    r = np.zeros((N, 1))
+    _, du, _ = O.dense_kkt(A, B, Q, R, M, r, np.diag(fam.wf), 0.0, x0)
+    assert np.max(np.abs(U - du)) < 1e-8

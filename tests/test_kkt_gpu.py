@@ -1,0 +1,160 @@
+"""GPU parity of the batched KKT scan (libnoc_hip.so) against the numpy oracle.
+
+Oracle: oracle/noc_oracle.kkt_solve, the restatement of seq_interior_point_newton bwd_pass /
+fwd_pass (noc/seq_interior_point_newton.py:42-90).  Tolerance (stated, fp64): max relative error
+1e-10 on dx, du, K, d, S, v and pred; `feasible` identical.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from lq_cases import rand_lq, oracle_batch  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-10
+
+
+def dev(x):
+    return None if x is None else torch.as_tensor(np.ascontiguousarray(x), dtype=torch.float64,
+                                                  device="cuda")
+
+
+def relerr(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def run_kkt(case, lanes, want_value=True):
+    from noc import lqt
+    g = lambda k: dev(case.get(k))
+    res = lqt.kkt_solve(g("A"), g("B"), g("Q"), g("R"), g("M"), g("r"), g("P"), reg=g("reg"),
+                        x0=g("x0"), q=g("q"), c=g("c"), p=g("p"), lanes=lanes,
+                        want_value=want_value)
+    torch.cuda.synchronize()
+    return {k: (None if v is None else v.cpu().numpy()) for k, v in res._asdict().items()}
+
+
+@pytest.mark.parametrize("nx,nu", [(2, 1), (4, 1), (8, 4)])
+@pytest.mark.parametrize("lanes", [64, 32, 16, 8])
+@pytest.mark.parametrize("N", [1, 7, 50, 200])
+@pytest.mark.parametrize("affine", [False, True])
+def test_kkt_matches_oracle(nx, nu, lanes, N, affine):
+    case = rand_lq(1000 * nx + N + lanes + int(affine), 5, N, nx, nu, affine=affine)
+    ref = oracle_batch(case)
+    out = run_kkt(case, lanes)
+    for k in ["dx", "du", "K", "d", "S", "v"]:
+        assert relerr(out[k], ref[k]) < RTOL, (k, relerr(out[k], ref[k]))
+    assert relerr(out["pred"], ref["pred"]) < RTOL
+    assert np.array_equal(out["feasible"].astype(bool), ref["feasible"].astype(bool))
+
+
+def test_kkt_infeasible_flag():
+    case = rand_lq(7, 4, 30, 4, 1)
+    case["R"][1, 10] = -50.0   # Quu < 0 at stage 10 of trajectory 1
+    case["R"][3, 29] = -50.0
+    ref = oracle_batch(case)
+    out = run_kkt(case, 64)
+    assert list(out["feasible"]) == [1, 0, 1, 0]
+    assert list(ref["feasible"].astype(int)) == [1, 0, 1, 0]
+    ok = [0, 2]
+    assert relerr(out["dx"][ok], ref["dx"][ok]) < RTOL
+
+
+def test_kkt_active_mask_leaves_inactive_untouched():
+    from noc import lqt
+    case = rand_lq(11, 6, 40, 4, 1)
+    g = lambda k: dev(case.get(k))
+    Bt, N = 6, 40
+    out = lqt.KKTResult(*(torch.full(s, 7.0, dtype=torch.float64, device="cuda") for s in
+                          [(Bt, N + 1, 4), (Bt, N, 1), (Bt,)]),
+                        torch.full((Bt,), 7, dtype=torch.int32, device="cuda"),
+                        torch.zeros(Bt, N, 1, 4, dtype=torch.float64, device="cuda"),
+                        torch.zeros(Bt, N, 1, dtype=torch.float64, device="cuda"), None, None)
+    active = torch.tensor([1, 0, 1, 0, 0, 1], dtype=torch.int32, device="cuda")
+    lqt.kkt_solve(g("A"), g("B"), g("Q"), g("R"), g("M"), g("r"), g("P"), reg=g("reg"),
+                  active=active, out=out)
+    torch.cuda.synchronize()
+    ref = oracle_batch(case)
+    dx = out.dx.cpu().numpy()
+    for b in range(Bt):
+        if active[b]:
+            assert relerr(dx[b], ref["dx"][b]) < RTOL
+        else:
+            assert np.all(dx[b] == 7.0) and out.pred[b].item() == 7.0
+
+
+@pytest.mark.parametrize("nx,nu", [(2, 1), (4, 1), (8, 4)])
+def test_split_bwd_fwd_entry_points(nx, nu):
+    from noc import lqt
+    case = rand_lq(5 + nx, 3, 37, nx, nu, affine=True)
+    g = lambda k: dev(case.get(k))
+    ref = oracle_batch(case)
+    K, d, S, v, pred, feas = lqt.bwd_pass(g("A"), g("B"), g("Q"), g("R"), g("M"), g("r"), g("P"),
+                                          reg=g("reg"), q=g("q"), c=g("c"), p=g("p"), lanes=16)
+    du, dx = lqt.fwd_pass(g("A"), g("B"), K, d, x0=g("x0"), c=g("c"), lanes=32)
+    torch.cuda.synchronize()
+    assert relerr(K.cpu(), ref["K"]) < RTOL
+    assert relerr(S.cpu(), ref["S"]) < RTOL
+    assert relerr(v.cpu(), ref["v"]) < RTOL
+    assert relerr(pred.cpu(), ref["pred"]) < RTOL
+    assert relerr(dx.cpu(), ref["dx"]) < RTOL
+    assert relerr(du.cpu(), ref["du"]) < RTOL
+
+
+def test_lqt_tracking_form_adapter():
+    """paroc LQT (LM:64) -> canonical -> HIP; compare with the oracle on the expanded form."""
+    from noc import lqt
+    from oracle import noc_oracle as O
+    rng = np.random.default_rng(3)
+    N, nx, nu = 25, 4, 1
+    case = rand_lq(3, 1, N, nx, nu)
+    H = np.eye(nx) + 0.1 * rng.normal(size=(N, nx, nx))
+    Z = np.ones((N, nu, nu))
+    rr = rng.normal(size=(N, nx))
+    ss = rng.normal(size=(N, nu))
+    X, U, Mt = case["Q"][0], case["R"][0], case["M"][0]
+    XT, HT, rT = case["P"][0], np.eye(nx), rng.normal(size=nx)
+    c = 0.1 * rng.normal(size=(N, nx))
+    x0 = rng.normal(size=nx)
+    L = lqt.LQT(*(dev(t) for t in (case["A"][0], case["B"][0], c, XT, HT, rT, X, H, rr, U, Z, ss, Mt)))
+    Kx, d, S, v, pred, feas = lqt.par_bwd_pass(L)
+    u, x = lqt.par_fwd_pass(L, dev(x0), Kx, d)
+    # expanded canonical form on the host
+    Q = np.einsum("kji,kjl,klm->kim", H, X, H)
+    M = np.einsum("kji,kjl,klm->kim", H, Mt, Z)
+    R = np.einsum("kji,kjl,klm->kim", Z, U, Z)
+    q = -np.einsum("kji,kj->ki", H, np.einsum("kij,kj->ki", X, rr) + np.einsum("kij,kj->ki", Mt, ss))
+    r = -np.einsum("kji,kj->ki", Z, np.einsum("kij,kj->ki", U, ss) + np.einsum("kji,kj->ki", Mt, rr))
+    P = HT.T @ XT @ HT
+    p = -HT.T @ XT @ rT
+    ddx, ddu, _ = O.dense_kkt(case["A"][0], case["B"][0], Q, R, M, r, P, 0.0, x0, q, c, p)
+    torch.cuda.synchronize()
+    assert relerr(x.cpu(), ddx) < 1e-9
+    assert relerr(u.cpu(), ddu) < 1e-9
+    assert bool(feas)
+
+
+def test_cartpole_blocks_full_size_properties():
+    """BASELINE config c3 size (N=200, B=4096): realistic cart-pole Newton blocks.
+    Checks (size-independent): dynamics consistency dx_{k+1} = A dx_k + B du_k exactly (to
+    rounding), oracle parity on a strided sample of 16 trajectories, all feasible."""
+    from noc import lqt
+    from noc.problems import make_bench_blocks
+    blocks = make_bench_blocks("cartpole", N=200, batch=4096, seed=0)
+    res = lqt.kkt_solve(blocks["A"], blocks["B"], blocks["Q"], blocks["R"], blocks["M"],
+                        blocks["r"], blocks["P"], reg=blocks["reg"])
+    torch.cuda.synchronize()
+    dx, du = res.dx, res.du
+    pred_dx = torch.einsum("bkij,bkj->bki", blocks["A"], dx[:, :-1]) + \
+        torch.einsum("bkij,bkj->bki", blocks["B"], du)
+    scale = dx.abs().max().item()
+    assert (pred_dx - dx[:, 1:]).abs().max().item() <= 1e-12 * max(1.0, scale)
+    sample = list(range(0, 4096, 256))
+    case = {k: blocks[k][sample].cpu().numpy() for k in ["A", "B", "Q", "R", "M", "r", "P", "reg"]}
+    ref = oracle_batch(case)
+    assert relerr(dx[sample].cpu(), ref["dx"]) < RTOL
+    assert relerr(du[sample].cpu(), ref["du"]) < RTOL
+    assert relerr(res.pred[sample].cpu(), ref["pred"]) < RTOL
+    assert bool(torch.all(res.feasible == 1))
