@@ -37,6 +37,10 @@ int noc_abi_version(void);
 const char* noc_last_error(void);
 int noc_kkt_supported(int nx, int nu);
 int noc_kkt_default_lanes(int nx, int nu, int N);
+/* Timing-only phase ablation of the KKT scan (bit0: skip the cross-lane scan, bit1: skip the
+ * forward pass, bit2: stop after the in-chunk elements).  Results are WRONG while set; used by
+ * tools/kkt_ablate.py to attribute kernel time to phases.  0 (default) in every product call. */
+void noc_debug_set_ablation(int bits);
 
 /* Fused batched KKT solve of one Newton step: par_bwd_pass + par_fwd_pass.
  * Replaces par_Newton's solver calls, noc/par_interior_point_newton.py:119-123

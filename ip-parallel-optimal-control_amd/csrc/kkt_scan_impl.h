@@ -302,8 +302,14 @@ __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(K
       prepend<NX, NU, AFF>(e, st);
     }
     // ---------------- phase 2: reverse Hillis-Steele across lanes ----------------
+    if (!(a.ablate & 1)) {
 #pragma unroll 1
-    for (int d = 1; d < L; d <<= 1) combine_shfl<NX>(e, d, L, l + d < L);
+      for (int d = 1; d < L; d <<= 1) combine_shfl<NX>(e, d, L, l + d < L);
+    }
+    if (a.ablate & 4) {  // phase 1 (+2) only: keep the element alive, skip the rest
+      if (a.pred) a.pred[traj] = e.J(0, 0) + e.A(0, 0) + e.C(0, 0) + e.nu[0] + e.b[0];
+      return;
+    }
     // ---------------- phase 3: in-chunk Riccati from the true boundary ----------------
     Sym<NX> S;
     Vec<NX> v;
@@ -435,7 +441,7 @@ __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(K
       if (a.pred) a.pred[traj] = pred;
       if (a.feasible) a.feasible[traj] = feas;
     }
-    if (a.mode == MODE_BWD) return;
+    if (a.mode == MODE_BWD || (a.ablate & 2)) return;
   } else {
     // MODE_FWD: gains are inputs; compose the chunk's closed-loop map from A, B, K, d
     set_identity(Phi);

@@ -10,6 +10,7 @@
 
 namespace {
 thread_local std::string g_last_error;
+int g_ablate = 0;  // timing-only phase ablation (noc_debug_set_ablation); never set in product use
 
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
@@ -64,6 +65,7 @@ int kkt_default_lanes(int nx, int nu, int N) {
 extern "C" {
 
 int noc_abi_version(void) { return NOC_ABI_VERSION; }
+void noc_debug_set_ablation(int bits) { g_ablate = bits; }
 const char* noc_last_error(void) { return g_last_error.c_str(); }
 int noc_kkt_supported(int nx, int nu) { return noc::kkt_supported(nx, nu) ? 1 : 0; }
 int noc_kkt_default_lanes(int nx, int nu, int N) { return noc::kkt_default_lanes(nx, nu, N); }
@@ -105,6 +107,7 @@ static int kkt_common(int mode, int nx, int nu, int N, int B, int lanes, const d
   a.P = P; a.p = p; a.x0 = x0; a.reg = reg; a.active = active;
   a.dx = dx; a.du = du; a.pred = pred; a.K = K; a.d = d; a.S = S; a.v = v;
   a.feasible = feasible;
+  a.ablate = g_ablate;
   (void)bwd;
   (void)fwd;
   const int L = lanes ? lanes : noc::kkt_default_lanes(nx, nu, N);

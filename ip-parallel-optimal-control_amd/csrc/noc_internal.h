@@ -15,6 +15,7 @@ struct KKTArgs {
   const int* active;
   double *dx, *du, *pred, *K, *d, *S, *v;
   int* feasible;
+  int ablate;  // timing-only ablation bits (tools/kkt_ablate.py); 0 in every product call
 };
 
 hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t stream);

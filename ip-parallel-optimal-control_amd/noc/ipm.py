@@ -73,8 +73,11 @@ class BatchedIPM:
         _lib.check(self._lib.noc_ipm_step(ctypes.byref(self.fam_c), ctypes.byref(self.ws), mode,
                                           terminal, self.lanes, self._stream()), "noc_ipm_step")
 
+    def active_count(self) -> int:
+        return int((self.t["phase"] != _lib.PHASE_DONE).sum().item())
+
     def all_done(self) -> bool:
-        return not bool(torch.any(self.t["phase"] != _lib.PHASE_DONE).item())
+        return self.active_count() == 0
 
     def solve(self, mode: int = _lib.MODE_PAR, terminal: int = _lib.TERMINAL_FINAL_COST,
               bp0: float = 0.1, poll_every: int = 8, max_steps: Optional[int] = None):

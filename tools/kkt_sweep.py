@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Time the KKT scan kernel per (config, lanes) -- interleaved rounds in one process (median of
+rounds), HIP events on the launch stream.  Prints one JSON line per variant."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ip-parallel-optimal-control_amd"))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {"c2": ("pendulum", 100, 1024), "c3": ("cartpole", 200, 4096),
+           "c4": ("linear8", 512, 16384), "c5": ("cartpole", 200, 8192)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c3,c2")
+    ap.add_argument("--lanes", default="64,32,16,8")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    from noc import lqt, problems
+    from bench import algorithmic_bytes
+    for cname in args.configs.split(","):
+        name, N, B = CONFIGS[cname]
+        blk = problems.make_bench_blocks(name, N=N, batch=B, seed=7)
+        nx, nu = blk["A"].shape[-1], blk["B"].shape[-1]
+        outs = {}
+        times = {int(L): [] for L in args.lanes.split(",")}
+        for L in times:
+            outs[L] = lqt.kkt_solve(blk["A"], blk["B"], blk["Q"], blk["R"], blk["M"], blk["r"],
+                                    blk["P"], reg=blk["reg"], lanes=L)
+        torch.cuda.synchronize()
+        ref = outs[64].dx
+        for _ in range(args.rounds):
+            for L in times:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.reps):
+                    lqt.kkt_solve(blk["A"], blk["B"], blk["Q"], blk["R"], blk["M"], blk["r"],
+                                  blk["P"], reg=blk["reg"], lanes=L, out=outs[L])
+                e1.record()
+                torch.cuda.synchronize()
+                times[L].append(e0.elapsed_time(e1) / args.reps)
+        abytes = algorithmic_bytes(nx, nu, N, B)
+        for L, ts in times.items():
+            ts = sorted(ts)
+            med = ts[len(ts) // 2]
+            diff = float((outs[L].dx - ref).abs().max())
+            print(json.dumps({"config": cname, "problem": name, "N": N, "B": B, "lanes": L,
+                              "ms_median": med, "ms_min": ts[0],
+                              "traj_kkt_per_s": B / (med * 1e-3),
+                              "achieved_GBs": abytes / (med * 1e-3) / 1e9,
+                              "max_abs_dx_diff_vs_L64": diff,
+                              "feasible_frac": float(outs[L].feasible.float().mean())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
