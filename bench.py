@@ -44,12 +44,14 @@ def pmc_traffic(path, kernel_substr):
 
 
 def cpu_baseline(blocks, sample, seconds=10.0):
-    """Time the C restatement of the sequential KKT solve on `sample` trajectories."""
-    import numpy as np
+    """Time the C restatement of the sequential KKT solve on `sample` trajectories (the same
+    blocks, relaid out to the natural layout)."""
     sys.path.insert(0, ROOT)
     from oracle import kkt_ref
-    idx = list(range(sample))
-    host = {k: blocks[k][idx].cpu().numpy() for k in ("A", "B", "Q", "R", "M", "r", "P", "reg")}
+    nat = blocks["engine"].natural_blocks()
+    nat["reg"] = blocks["reg"]
+    host = {k: nat[k][:sample].cpu().numpy() for k in ("A", "B", "Q", "R", "M", "r", "P", "reg")}
+    del nat
     cores = len(os.sched_getaffinity(0))
     cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
     kkt_ref.solve(*(host[k] for k in ("A", "B", "Q", "R", "M", "r", "P", "reg")), threads=cores)
@@ -72,6 +74,8 @@ def main():
     ap.add_argument("--horizon", type=int, default=200)
     ap.add_argument("--batch", type=int, default=4096, help="trajectories per GPU")
     ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--layout", choices=["tiled", "natural"], default="tiled",
+                    help="HBM layout of the LQ blocks (tiled = what the linearisation kernels write)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-sample", type=int, default=512)
     ap.add_argument("--no-cpu", action="store_true")
@@ -89,15 +93,21 @@ def main():
     from noc import lqt, problems, _lib
 
     N, B = args.horizon, args.batch
-    blocks = problems.make_bench_blocks(args.problem, N=N, batch=B, seed=1234 + rank)
-    nx, nu = blocks["A"].shape[-1], blocks["B"].shape[-1]
-    lanes = args.lanes or _lib.load().noc_kkt_default_lanes(nx, nu, N)
-    out = lqt.kkt_solve(blocks["A"], blocks["B"], blocks["Q"], blocks["R"], blocks["M"],
-                        blocks["r"], blocks["P"], reg=blocks["reg"], lanes=lanes)
+    blocks = problems.make_bench_blocks(args.problem, N=N, batch=B, seed=1234 + rank,
+                                        lanes=args.lanes, natural=(args.layout == "natural"))
+    tb = blocks["tiled"]
+    nx, nu, lanes = tb.nx, tb.nu, tb.lanes
+    if args.layout == "tiled":
+        out = lqt.kkt_solve_tiled(tb, reg=blocks["reg"])
 
-    def step():
-        lqt.kkt_solve(blocks["A"], blocks["B"], blocks["Q"], blocks["R"], blocks["M"], blocks["r"],
-                      blocks["P"], reg=blocks["reg"], lanes=lanes, out=out)
+        def step():
+            lqt.kkt_solve_tiled(tb, reg=blocks["reg"], out=out)
+    else:
+        nat = [blocks[k] for k in ("A", "B", "Q", "R", "M", "r", "P")]
+        out = lqt.kkt_solve(*nat, reg=blocks["reg"], lanes=lanes)
+
+        def step():
+            lqt.kkt_solve(*nat, reg=blocks["reg"], lanes=lanes, out=out)
 
     for _ in range(args.warmup):
         step()
@@ -143,6 +153,7 @@ def main():
                 "linearised on device",
         "config": {"workload": f"{args.problem} nx={nx} nu={nu} N={N} batch={B}/GPU "
                                f"(BASELINE c3; c5 when run on 8 GPUs)",
+                   "layout": args.layout,
                    "horizon": N, "batch_per_gpu": B, "global_batch": B * world,
                    "lanes_per_trajectory": lanes, "parallelism": f"trajectory-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -53,6 +53,29 @@ int noc_kkt_solve(int nx, int nu, int N, int B, int lanes,
                   double* dx, double* du, double* pred, int* feasible,
                   double* K, double* d, double* S, double* v, void* stream);
 
+/* ---- tiled ("lane-interleaved") block layout ------------------------------------------------
+ * For `lanes` = L lanes per trajectory, stage s of an N-stage horizon belongs to chunk lane l at
+ * chunk position j (lanes l < N % L own N/L + 1 stages, the others N/L; chunks are contiguous in
+ * time, cmax = ceil(N/L)).  A field with E doubles per stage is stored, per trajectory b, as
+ *   E even: [b][j][e/2][l][2]      E odd: [b][j][e][l]
+ * (noc_tiled_doubles() doubles per field).  Q and R are stored PACKED symmetric (upper triangle,
+ * row-major: E = n(n+1)/2).  Every wave-wide access of the KKT scan is then L*16 contiguous
+ * bytes.  The interior-point workspace (noc_ipm_ws) always uses this layout. */
+long long noc_tiled_doubles(int N, int B, int lanes, int E);
+/* direction 0: natural (B,N,E) -> tiled; 1: tiled -> natural.  sym_n > 0: the natural field is a
+ * full sym_n x sym_n matrix per stage and the tiled one packed (E must be sym_n(sym_n+1)/2). */
+int noc_relayout(int direction, int E, int sym_n, int N, int B, int lanes, const double* src,
+                 double* dst, void* stream);
+/* noc_kkt_solve with A, Bm, Q(packed), R(packed), M, r, q, c, K, d in the tiled layout of
+ * `lanes` (required, 8/16/32/64); P, p, x0, reg, dx, du, S, v natural. */
+int noc_kkt_solve_tiled(int nx, int nu, int N, int B, int lanes,
+                        const double* A, const double* Bm, const double* Q, const double* R,
+                        const double* M, const double* r, const double* q, const double* c,
+                        const double* P, const double* p, const double* x0, const double* reg,
+                        const int* active,
+                        double* dx, double* du, double* pred, int* feasible,
+                        double* K, double* d, double* S, double* v, void* stream);
+
 /* Backward pass only: replaces paroc.par_bwd_pass (call sites
  * noc/par_interior_point_newton.py:120, examples/linear_mpc_parallel.py:68). */
 int noc_par_bwd_pass(int nx, int nu, int N, int B, int lanes,
@@ -107,10 +130,12 @@ typedef struct noc_family {
 /* Workspace of device pointers (all fp64 unless noted; Bt trajectories, horizon N). */
 typedef struct noc_ipm_ws {
   int Bt, N;
+  int lanes;                           /* tiled layout of A,B,Q,R,M,r,K,d (8/16/32/64)  */
+  int reserved;
   double *x, *u, *x0;                  /* (Bt,N+1,nx) (Bt,N,nu) (Bt,nx)           */
-  double *A, *B, *Q, *R, *M, *r, *P;   /* LQ blocks, layouts as noc_kkt_solve      */
+  double *A, *B, *Q, *R, *M, *r, *P;   /* LQ blocks: tiled (P natural)              */
   double *cx, *cu, *lc, *lam;          /* (Bt,N,nx) (Bt,N,nu) (Bt,N) (Bt,N+1,nx)    */
-  double *dx, *du, *pred, *K, *d;      /* KKT outputs                              */
+  double *dx, *du, *pred, *K, *d;      /* KKT outputs (dx, du natural; K, d tiled)  */
   int *feasible;                       /* (Bt) int32                               */
   int *phase, *kkt_active, *it, *inner, *total_it, *kkt_solves; /* (Bt) int32     */
   double *bp, *rp, *rinc, *cost, *hu, *gnorm, *reg;              /* (Bt)           */

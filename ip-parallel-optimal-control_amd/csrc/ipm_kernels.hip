@@ -155,26 +155,32 @@ __global__ __launch_bounds__(256) void rollout_kernel(noc_family prm, noc_ipm_ws
   w.phase[b] = NOC_PHASE_LINEARIZE;
 }
 
+// thread per (trajectory, chunk slot, lane) in tiled order: the A/B stores are coalesced
 template <int KIND, int NX, int NU>
 __global__ __launch_bounds__(256) void linearize_kernel(noc_family prm, noc_ipm_ws w) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int N = w.N;
-  if (t >= (long long)w.Bt * N) return;
-  const int b = (int)(t / N), k = (int)(t % N);
-  if (w.phase[b] != NOC_PHASE_LINEARIZE) return;
+  const int N = w.N, L = w.lanes;
+  const Chunks ch(N, L);
+  if (t >= (long long)w.Bt * ch.cmax * L) return;
+  const int b = (int)(t / ((long long)ch.cmax * L));
+  const int rem = (int)(t % ((long long)ch.cmax * L));
+  const int j = rem / L, l = rem % L;
+  if (j >= ch.len(l) || w.phase[b] != NOC_PHASE_LINEARIZE) return;
+  const int k = ch.start(l) + j;
+  const size_t tn = (size_t)b * N + k;
   Fam<KIND, NX, NU> f(prm);
   const double bp = w.bp[b];
   double x[NX], u[NU];
   gload<NX>(w.x + ((size_t)b * (N + 1) + k) * NX, x);
-  NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = w.u[(size_t)t * NU + j];
+  NOC_UNROLL for (int i = 0; i < NU; ++i) u[i] = w.u[tn * NU + i];
   double fx[NX * NX], fu[NX * NU], cx[NX], cu[NU];
   f.jac(x, u, fx, fu);
   f.stage_grad(x, u, bp, cx, cu);
-  gstore<NX * NX>(w.A + (size_t)t * NX * NX, fx);
-  gstore<NX * NU>(w.B + (size_t)t * NX * NU, fu);
-  gstore<NX>(w.cx + (size_t)t * NX, cx);
-  NOC_UNROLL for (int j = 0; j < NU; ++j) w.cu[(size_t)t * NU + j] = cu[j];
-  w.lc[t] = f.stage_cost(x, u, bp);
+  tstore_rt<NX * NX>(w.A, L, ch.cmax, b, j, l, fx);
+  tstore_rt<NX * NU>(w.B, L, ch.cmax, b, j, l, fu);
+  gstore<NX>(w.cx + tn * NX, cx);
+  NOC_UNROLL for (int i = 0; i < NU; ++i) w.cu[tn * NU + i] = cu[i];
+  w.lc[tn] = f.stage_cost(x, u, bp);
 }
 
 // one thread per trajectory: sequential costate recursion (C:43-54) + per-trajectory scalars
@@ -185,6 +191,7 @@ __global__ __launch_bounds__(256) void costate_kernel(noc_family prm, noc_ipm_ws
   Fam<KIND, NX, NU> f(prm);
   const int N = w.N;
   const size_t bN = (size_t)b * N;
+  const Chunks ch(N, w.lanes);
   const double* xN = w.x + ((size_t)b * (N + 1) + N) * NX;
   double xf[NX], lam[NX];
   NOC_UNROLL for (int i = 0; i < NX; ++i) xf[i] = xN[i];
@@ -199,19 +206,22 @@ __global__ __launch_bounds__(256) void costate_kernel(noc_family prm, noc_ipm_ws
   double hu = 0.0, g2 = 0.0;
   for (int k = N - 1; k >= 0; --k) {
     const size_t t = bN + k;
-    double A[NX * NX], Bm[NX * NU], cx[NX];
-    gload<NX * NX>(w.A + t * NX * NX, A);
-    gload<NX * NU>(w.B + t * NX * NU, Bm);
+    double A[NX * NX], Bm[NX * NU], cx[NX], rr[NU];
+    int l, j;
+    ch.owner(k, l, j);
+    tload_rt<NX * NX>(w.A, w.lanes, ch.cmax, b, j, l, A);
+    tload_rt<NX * NU>(w.B, w.lanes, ch.cmax, b, j, l, Bm);
     gload<NX>(w.cx + t * NX, cx);
     // ru_k = cu_k + fu_k' lambda_{k+1}  (P:34)
-    NOC_UNROLL for (int j = 0; j < NU; ++j) {
-      const double cu = w.cu[t * NU + j];
+    NOC_UNROLL for (int jj = 0; jj < NU; ++jj) {
+      const double cu = w.cu[t * NU + jj];
       double r = cu;
-      NOC_UNROLL for (int i = 0; i < NX; ++i) r += Bm[i * NU + j] * lam[i];
-      w.r[t * NU + j] = r;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) r += Bm[i * NU + jj] * lam[i];
+      rr[jj] = r;
       hu = fmax(hu, fabs(r));
       g2 += cu * cu;
     }
+    tstore_rt<NU>(w.r, w.lanes, ch.cmax, b, j, l, rr);
     double ln[NX];
     NOC_UNROLL for (int i = 0; i < NX; ++i) {
       double s = cx[i];
@@ -233,25 +243,36 @@ __global__ __launch_bounds__(256) void costate_kernel(noc_family prm, noc_ipm_ws
 template <int KIND, int NX, int NU>
 __global__ __launch_bounds__(256) void assemble_kernel(noc_family prm, noc_ipm_ws w, int terminal) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int N = w.N;
-  if (t >= (long long)w.Bt * N) return;
-  const int b = (int)(t / N), k = (int)(t % N);
-  if (w.phase[b] != NOC_PHASE_LINEARIZE) return;
+  const int N = w.N, L = w.lanes;
+  const Chunks ch(N, L);
+  if (t >= (long long)w.Bt * ch.cmax * L) return;
+  const int b = (int)(t / ((long long)ch.cmax * L));
+  const int rem = (int)(t % ((long long)ch.cmax * L));
+  const int j = rem / L, l = rem % L;
+  if (j >= ch.len(l) || w.phase[b] != NOC_PHASE_LINEARIZE) return;
+  const int k = ch.start(l) + j;
+  const size_t tn = (size_t)b * N + k;
   Fam<KIND, NX, NU> f(prm);
   const double bp = w.bp[b];
   double x[NX], u[NU], lam[NX];
   gload<NX>(w.x + ((size_t)b * (N + 1) + k) * NX, x);
-  NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = w.u[(size_t)t * NU + j];
+  NOC_UNROLL for (int i = 0; i < NU; ++i) u[i] = w.u[tn * NU + i];
   gload<NX>(w.lam + ((size_t)b * (N + 1) + k + 1) * NX, lam);
   // Q = cxx + l.fxx ; R = cuu + l.fuu ; M = cxu + l.fxu  (P:35-37), l = lambda_{k+1}
   double Q[NX * NX], R[NU * NU], M[NX * NU];
-  NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) Q[i * NX + j] = (i == j) ? prm.wx[i] : 0.0;
-  NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int j = 0; j < NU; ++j) R[i * NU + j] = (i == j) ? f.stage_cuu(u, bp, i) : 0.0;
+  NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int jj = 0; jj < NX; ++jj) Q[i * NX + jj] = (i == jj) ? prm.wx[i] : 0.0;
+  NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int jj = 0; jj < NU; ++jj) R[i * NU + jj] = (i == jj) ? f.stage_cuu(u, bp, i) : 0.0;
   NOC_UNROLL for (int i = 0; i < NX * NU; ++i) M[i] = 0.0;
   f.add_hess_l(x, u, lam, Q, R, M);
-  gstore<NX * NX>(w.Q + (size_t)t * NX * NX, Q);
-  gstore<NU * NU>(w.R + (size_t)t * NU * NU, R);
-  gstore<NX * NU>(w.M + (size_t)t * NX * NU, M);
+  Sym<NX> Qs;
+  Sym<NU> Rs;
+  NOC_UNROLL for (int i = 0; i < NX; ++i)
+    NOC_UNROLL for (int jj = i; jj < NX; ++jj) Qs(i, jj) = (i == jj) ? Q[i * NX + i] : 0.5 * (Q[i * NX + jj] + Q[jj * NX + i]);
+  NOC_UNROLL for (int i = 0; i < NU; ++i)
+    NOC_UNROLL for (int jj = i; jj < NU; ++jj) Rs(i, jj) = (i == jj) ? R[i * NU + i] : 0.5 * (R[i * NU + jj] + R[jj * NU + i]);
+  tstore_rt<Sym<NX>::SZ>(w.Q, L, ch.cmax, b, j, l, Qs.v);
+  tstore_rt<Sym<NU>::SZ>(w.R, L, ch.cmax, b, j, l, Rs.v);
+  tstore_rt<NX * NU>(w.M, L, ch.cmax, b, j, l, M);
   if (terminal == NOC_TERMINAL_STAGE0 && k == 0) gstore<NX * NX>(w.P + (size_t)b * NX * NX, Q);  // P:73
 }
 
@@ -376,7 +397,8 @@ template <int KIND, int NX, int NU>
 static hipError_t prepare_t(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                             hipStream_t s) {
   const int bt_grid = (w.Bt + 255) / 256;
-  const unsigned st_grid = (unsigned)(((long long)w.Bt * w.N + 255) / 256);
+  const long long cmax = (w.N + w.lanes - 1) / w.lanes;
+  const unsigned st_grid = (unsigned)(((long long)w.Bt * cmax * w.lanes + 255) / 256);
   hipLaunchKernelGGL((rollout_kernel<KIND, NX, NU>), dim3(bt_grid), dim3(256), 0, s, p, w);
   hipLaunchKernelGGL((linearize_kernel<KIND, NX, NU>), dim3(st_grid), dim3(256), 0, s, p, w);
   hipLaunchKernelGGL((costate_kernel<KIND, NX, NU>), dim3(bt_grid), dim3(256), 0, s, p, w, mode);

@@ -54,18 +54,70 @@ struct Elem {
   Sym<NX> J;
 };
 
-template <int NX, int NU, bool AFF>
-NOC_DEV void load_stage(const KKTArgs& a, size_t si, double reg, StageData<NX, NU>& st) {
-  gload<NX * NX>(a.A + si * (NX * NX), st.A.v);
-  gload<NX * NU>(a.Bm + si * (NX * NU), st.B.v);
-  gload_sym<NX>(a.Q + si * (NX * NX), st.Q);
-  gload_sym<NU>(a.R + si * (NU * NU), st.R);
+template <int NX, int NU, int L, bool AFF, bool TILED>
+NOC_DEV void load_stage(const KKTArgs& a, int traj, size_t si, int j, int l, int cmax, double reg,
+                        StageData<NX, NU>& st) {
+  if constexpr (TILED) {
+    tload<NX * NX, L>(a.A, traj, j, l, cmax, st.A.v);
+    tload<NX * NU, L>(a.Bm, traj, j, l, cmax, st.B.v);
+    tload<Sym<NX>::SZ, L>(a.Q, traj, j, l, cmax, st.Q.v);
+    tload<Sym<NU>::SZ, L>(a.R, traj, j, l, cmax, st.R.v);
+    tload<NX * NU, L>(a.M, traj, j, l, cmax, st.M.v);
+    tload<NU, L>(a.r, traj, j, l, cmax, st.r.v);
+    if constexpr (AFF) {
+      if (a.q) tload<NX, L>(a.q, traj, j, l, cmax, st.q.v); else set_zero(st.q);
+      if (a.c) tload<NX, L>(a.c, traj, j, l, cmax, st.c.v); else set_zero(st.c);
+    }
+  } else {
+    gload<NX * NX>(a.A + si * (NX * NX), st.A.v);
+    gload<NX * NU>(a.Bm + si * (NX * NU), st.B.v);
+    gload_sym<NX>(a.Q + si * (NX * NX), st.Q);
+    gload_sym<NU>(a.R + si * (NU * NU), st.R);
+    gload<NX * NU>(a.M + si * (NX * NU), st.M.v);
+    gload<NU>(a.r + si * NU, st.r.v);
+    if constexpr (AFF) {
+      if (a.q) gload<NX>(a.q + si * NX, st.q.v); else set_zero(st.q);
+      if (a.c) gload<NX>(a.c + si * NX, st.c.v); else set_zero(st.c);
+    }
+  }
   NOC_UNROLL for (int i = 0; i < NU; ++i) st.R(i, i) += reg;
-  gload<NX * NU>(a.M + si * (NX * NU), st.M.v);
-  gload<NU>(a.r + si * NU, st.r.v);
-  if constexpr (AFF) {
-    if (a.q) gload<NX>(a.q + si * NX, st.q.v); else set_zero(st.q);
-    if (a.c) gload<NX>(a.c + si * NX, st.c.v); else set_zero(st.c);
+}
+
+// A, B (and c) of one stage for the forward pass / map composition
+template <int NX, int NU, int L, bool AFF, bool TILED>
+NOC_DEV void load_AB(const KKTArgs& a, int traj, size_t si, int j, int l, int cmax,
+                     Mat<NX, NX>& A, Mat<NX, NU>& Bm, Vec<NX>& c) {
+  set_zero(c);
+  if constexpr (TILED) {
+    tload<NX * NX, L>(a.A, traj, j, l, cmax, A.v);
+    tload<NX * NU, L>(a.Bm, traj, j, l, cmax, Bm.v);
+    if constexpr (AFF) { if (a.c) tload<NX, L>(a.c, traj, j, l, cmax, c.v); }
+  } else {
+    gload<NX * NX>(a.A + si * (NX * NX), A.v);
+    gload<NX * NU>(a.Bm + si * (NX * NU), Bm.v);
+    if constexpr (AFF) { if (a.c) gload<NX>(a.c + si * NX, c.v); }
+  }
+}
+
+// gains K (NU x NX) followed by d (NU), packed as Kk[NU*(NX+1)]
+template <int NX, int NU, int L, bool TILED>
+NOC_DEV void store_Kd(const KKTArgs& a, int traj, size_t si, int j, int l, int cmax, const double* Kk) {
+  if constexpr (TILED) {
+    tstore<NU * NX, L>(a.K, traj, j, l, cmax, Kk);
+    tstore<NU, L>(a.d, traj, j, l, cmax, Kk + NU * NX);
+  } else {
+    gstore<NU * NX>(a.K + si * (NU * NX), Kk);
+    gstore<NU>(a.d + si * NU, Kk + NU * NX);
+  }
+}
+template <int NX, int NU, int L, bool TILED>
+NOC_DEV void load_Kd(const KKTArgs& a, int traj, size_t si, int j, int l, int cmax, double* Kk) {
+  if constexpr (TILED) {
+    tload<NU * NX, L>(a.K, traj, j, l, cmax, Kk);
+    tload<NU, L>(a.d, traj, j, l, cmax, Kk + NU * NX);
+  } else {
+    gload<NU * NX>(a.K + si * (NU * NX), Kk);
+    gload<NU>(a.d + si * NU, Kk + NU * NX);
   }
 }
 
@@ -175,34 +227,39 @@ NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st) {
 }
 
 // e1 <- e1 (x) e2  (e1 covers the earlier interval, e2 = the partner lane's element, later one).
-// Partner fields arrive in two shuffle batches so that at most one half of e2 is live at a time;
-// lanes without a partner (l + d >= L) get the identity element (I, 0, 0, 0, 0), for which the
-// combine is exact, so the whole segment runs one uniform instruction stream (no divergent
-// ds_bpermute: a shuffle never reads an EXEC-masked lane).
-template <int NX>
-NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L, bool valid) {
+// Partner fields arrive by ds_bpermute in two batches so that at most one half of e2 is live at a
+// time.  Lanes without a partner (l + d >= L) receive their OWN element (__shfl_down width
+// semantics); such a lane already covers the suffix up to the terminal cost, so its element is
+// value-only (A = b = C = 0) and e (x) e == e exactly -- no selects, one uniform instruction
+// stream, and no shuffle ever reads an EXEC-masked lane.
+// VALUE_ONLY: every right operand is value-only (the last level: partner l + L/2 covers the end),
+// so the result is value-only too and only J, nu are formed (T A1 is the only solve needed).
+template <int NX, bool VALUE_ONLY>
+NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
   Sym<NX> J2;
   Vec<NX> nu2;
   shfl_down_arr<Sym<NX>::SZ>(e1.J.v, J2.v, d, L);
   shfl_down_arr<NX>(e1.nu.v, nu2.v, d, L);
-  NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) J2.v[i] = valid ? J2.v[i] : 0.0;
-  NOC_UNROLL for (int i = 0; i < NX; ++i) nu2.v[i] = valid ? nu2.v[i] : 0.0;
-
+  constexpr int NR = VALUE_ONLY ? NX : 2 * NX + 1;
   double X[NX][NX];
-  constexpr int NR = 2 * NX + 1;
   double Y[NX][NR];
-  NOC_UNROLL for (int i = 0; i < NX; ++i) {
-    NOC_UNROLL for (int j = 0; j < NX; ++j) {
-      double s = (i == j) ? 1.0 : 0.0;
-      NOC_UNROLL for (int k = 0; k < NX; ++k) s += e1.C(i, k) * J2(k, j);
-      X[i][j] = s;
-      Y[i][j] = e1.A(i, j);
-      Y[i][NX + 1 + j] = e1.C(i, j);
+  auto build = [&]() {
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      NOC_UNROLL for (int j = 0; j < NX; ++j) {
+        double s = (i == j) ? 1.0 : 0.0;
+        NOC_UNROLL for (int k = 0; k < NX; ++k) s += e1.C(i, k) * J2(k, j);
+        X[i][j] = s;
+        Y[i][j] = e1.A(i, j);
+        if constexpr (!VALUE_ONLY) Y[i][NX + 1 + j] = e1.C(i, j);
+      }
+      if constexpr (!VALUE_ONLY) {
+        double s = e1.b[i];
+        NOC_UNROLL for (int k = 0; k < NX; ++k) s -= e1.C(i, k) * nu2[k];
+        Y[i][NX] = s;
+      }
     }
-    double s = e1.b[i];
-    NOC_UNROLL for (int k = 0; k < NX; ++k) s -= e1.C(i, k) * nu2[k];
-    Y[i][NX] = s;
-  }
+  };
+  build();
   //  J2A1 = J2 A1,  w = nu2 + J2 b1   (e1.A, e1.b are still the pre-combine values)
   Mat<NX, NX> J2A1;
   Vec<NX> w;
@@ -216,7 +273,12 @@ NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L, bool valid) {
       J2A1(i, j) = s;
     }
   }
-  lu_pp_solve<NX, NR>(X, Y);  // Y = [TA | Tb | TC],  T = (I + C1 J2)^-1
+  // Y = [TA | Tb | TC],  T = (I + C1 J2)^-1: threshold-checked solve without row exchanges,
+  // partial pivoting for the (rare) lanes whose check fails
+  if (!lu_np_solve<NX, NR>(X, Y)) {
+    build();
+    lu_pp_solve<NX, NR>(X, Y);
+  }
   // J = J1 + TA' J2 A1 ; nu = nu1 + TA' w
   NOC_UNROLL for (int i = 0; i < NX; ++i) {
     NOC_UNROLL for (int j = i; j < NX; ++j) {
@@ -228,42 +290,44 @@ NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L, bool valid) {
     NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * w[k];
     e1.nu[i] = s;
   }
-  // second batch: partner's A, b, C (not yet modified by any lane at this level)
-  Mat<NX, NX> A2;
-  Vec<NX> b2;
-  Sym<NX> C2;
-  shfl_down_arr<NX * NX>(e1.A.v, A2.v, d, L);
-  shfl_down_arr<NX>(e1.b.v, b2.v, d, L);
-  shfl_down_arr<Sym<NX>::SZ>(e1.C.v, C2.v, d, L);
-  NOC_UNROLL for (int i = 0; i < NX; ++i)
-    NOC_UNROLL for (int j = 0; j < NX; ++j) A2(i, j) = valid ? A2(i, j) : (i == j ? 1.0 : 0.0);
-  NOC_UNROLL for (int i = 0; i < NX; ++i) b2.v[i] = valid ? b2.v[i] : 0.0;
-  NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) C2.v[i] = valid ? C2.v[i] : 0.0;
-  // A = A2 TA ; b = A2 Tb + b2 ; C = A2 TC A2' + C2
-  Mat<NX, NX> T2;  // A2 * TC
-  NOC_UNROLL for (int i = 0; i < NX; ++i) {
-    double sb = b2[i];
-    NOC_UNROLL for (int k = 0; k < NX; ++k) sb += A2(i, k) * Y[k][NX];
-    e1.b[i] = sb;
-    NOC_UNROLL for (int j = 0; j < NX; ++j) {
-      double sa = 0.0, st = 0.0;
-      NOC_UNROLL for (int k = 0; k < NX; ++k) {
-        sa += A2(i, k) * Y[k][j];
-        st += A2(i, k) * Y[k][NX + 1 + j];
+  if constexpr (VALUE_ONLY) {
+    set_zero(e1.A);
+    set_zero(e1.b);
+    set_zero(e1.C);
+  } else {
+    // second batch: partner's A, b, C (not yet modified by any lane at this level)
+    Mat<NX, NX> A2;
+    Vec<NX> b2;
+    Sym<NX> C2;
+    shfl_down_arr<NX * NX>(e1.A.v, A2.v, d, L);
+    shfl_down_arr<NX>(e1.b.v, b2.v, d, L);
+    shfl_down_arr<Sym<NX>::SZ>(e1.C.v, C2.v, d, L);
+    // A = A2 TA ; b = A2 Tb + b2 ; C = A2 TC A2' + C2
+    Mat<NX, NX> T2;  // A2 * TC
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      double sb = b2[i];
+      NOC_UNROLL for (int k = 0; k < NX; ++k) sb += A2(i, k) * Y[k][NX];
+      e1.b[i] = sb;
+      NOC_UNROLL for (int j = 0; j < NX; ++j) {
+        double sa = 0.0, st = 0.0;
+        NOC_UNROLL for (int k = 0; k < NX; ++k) {
+          sa += A2(i, k) * Y[k][j];
+          st += A2(i, k) * Y[k][NX + 1 + j];
+        }
+        e1.A(i, j) = sa;
+        T2(i, j) = st;
       }
-      e1.A(i, j) = sa;
-      T2(i, j) = st;
     }
+    NOC_UNROLL for (int i = 0; i < NX; ++i)
+      NOC_UNROLL for (int j = i; j < NX; ++j) {
+        double s = C2(i, j);
+        NOC_UNROLL for (int k = 0; k < NX; ++k) s += T2(i, k) * A2(j, k);
+        e1.C(i, j) = s;
+      }
   }
-  NOC_UNROLL for (int i = 0; i < NX; ++i)
-    NOC_UNROLL for (int j = i; j < NX; ++j) {
-      double s = C2(i, j);
-      NOC_UNROLL for (int k = 0; k < NX; ++k) s += T2(i, k) * A2(j, k);
-      e1.C(i, j) = s;
-    }
 }
 
-template <int NX, int NU, int L, bool AFF>
+template <int NX, int NU, int L, bool AFF, bool TILED>
 __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int traj = tid / L;
@@ -277,6 +341,7 @@ __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(K
   const bool last = (l == L - 1);
   const double reg = a.reg ? a.reg[traj] : 0.0;
   const size_t tN = (size_t)traj * N;
+  const int cmax = base + (rem ? 1 : 0);
 
 
   Mat<NX, NX> Phi;
@@ -298,13 +363,14 @@ __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(K
     }
     for (int s = start + len - 1; s >= start; --s) {
       StageData<NX, NU> st;
-      load_stage<NX, NU, AFF>(a, tN + s, reg, st);
+      load_stage<NX, NU, L, AFF, TILED>(a, traj, tN + s, s - start, l, cmax, reg, st);
       prepend<NX, NU, AFF>(e, st);
     }
     // ---------------- phase 2: reverse Hillis-Steele across lanes ----------------
     if (!(a.ablate & 1)) {
 #pragma unroll 1
-      for (int d = 1; d < L; d <<= 1) combine_shfl<NX>(e, d, L, l + d < L);
+      for (int d = 1; d < L / 2; d <<= 1) combine_shfl<NX, false>(e, d, L);
+      combine_shfl<NX, true>(e, L / 2, L);  // last level: all right operands are value-only
     }
     if (a.ablate & 4) {  // phase 1 (+2) only: keep the element alive, skip the rest
       if (a.pred) a.pred[traj] = e.J(0, 0) + e.A(0, 0) + e.C(0, 0) + e.nu[0] + e.b[0];
@@ -328,7 +394,7 @@ __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(K
     int feas = 1;
     for (int s = start + len - 1; s >= start; --s) {
       StageData<NX, NU> st;
-      load_stage<NX, NU, AFF>(a, tN + s, reg, st);
+      load_stage<NX, NU, L, AFF, TILED>(a, traj, tN + s, s - start, l, cmax, reg, st);
       Mat<NX, NX> SA;
       Mat<NX, NU> SB;
       NOC_UNROLL for (int i = 0; i < NX; ++i) {
@@ -379,8 +445,7 @@ __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(K
         NOC_UNROLL for (int j = 0; j < NX; ++j) Kk[i * NX + j] = -Y[i][j];
         Kk[NU * NX + i] = -Y[i][NX];
       }
-      gstore<NU * NX>(a.K + (tN + s) * (NU * NX), Kk);
-      gstore<NU>(a.d + (tN + s) * NU, Kk + NU * NX);
+      store_Kd<NX, NU, L, TILED>(a, traj, tN + s, s - start, l, cmax, Kk);
       // dV = k'Qu + 1/2 k'Quu k   (noc/seq_interior_point_newton.py:63)
       NOC_UNROLL for (int i = 0; i < NU; ++i) {
         const double ki = Kk[NU * NX + i];
@@ -450,13 +515,9 @@ __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(K
       Mat<NX, NX> A;
       Mat<NX, NU> Bm;
       double Kk[NU * (NX + 1)];
-      gload<NX * NX>(a.A + (tN + s) * (NX * NX), A.v);
-      gload<NX * NU>(a.Bm + (tN + s) * (NX * NU), Bm.v);
-      gload<NU * NX>(a.K + (tN + s) * (NU * NX), Kk);
-      gload<NU>(a.d + (tN + s) * NU, Kk + NU * NX);
       Vec<NX> cc;
-      set_zero(cc);
-      if constexpr (AFF) { if (a.c) gload<NX>(a.c + (tN + s) * NX, cc.v); }
+      load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + s, s - start, l, cmax, A, Bm, cc);
+      load_Kd<NX, NU, L, TILED>(a, traj, tN + s, s - start, l, cmax, Kk);
       Mat<NX, NX> F;
       Vec<NX> f;
       NOC_UNROLL for (int i = 0; i < NX; ++i) {
@@ -502,11 +563,8 @@ __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(K
     Vec<NX> op;
     shfl_up_arr<NX * NX>(Phi.v, oP.v, d, L);
     shfl_up_arr<NX>(phi.v, op.v, d, L);
-    const bool valid = l >= d;  // identity map for lanes without a predecessor at this level
-    NOC_UNROLL for (int i = 0; i < NX; ++i) {
-      op[i] = valid ? op[i] : 0.0;
-      NOC_UNROLL for (int j = 0; j < NX; ++j) oP(i, j) = valid ? oP(i, j) : (i == j ? 1.0 : 0.0);
-    }
+    // lanes l < d get their own map back (__shfl_up width semantics); their prefix already starts
+    // at lane 0, whose map is constant (Phi = 0), so composing with it changes nothing.
     Mat<NX, NX> Pn;
     NOC_UNROLL for (int i = 0; i < NX; ++i) {
       double t = phi[i];
@@ -527,10 +585,9 @@ __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(K
     Mat<NX, NX> A;
     Mat<NX, NU> Bm;
     double Kk[NU * (NX + 1)];
-    gload<NX * NX>(a.A + (tN + s) * (NX * NX), A.v);
-    gload<NX * NU>(a.Bm + (tN + s) * (NX * NU), Bm.v);
-    gload<NU * NX>(a.K + (tN + s) * (NU * NX), Kk);
-    gload<NU>(a.d + (tN + s) * NU, Kk + NU * NX);
+    Vec<NX> cc;
+    load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + s, s - start, l, cmax, A, Bm, cc);
+    load_Kd<NX, NU, L, TILED>(a, traj, tN + s, s - start, l, cmax, Kk);
     Vec<NU> u;
     NOC_UNROLL for (int i = 0; i < NU; ++i) {
       double t = Kk[NU * NX + i];
@@ -541,8 +598,7 @@ __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(K
     if (a.du) gstore<NU>(a.du + (tN + s) * NU, u.v);
     Vec<NX> xn;
     NOC_UNROLL for (int i = 0; i < NX; ++i) {
-      double t = 0.0;
-      if constexpr (AFF) { if (a.c) t = a.c[(tN + s) * NX + i]; }
+      double t = cc[i];
       NOC_UNROLL for (int k = 0; k < NX; ++k) t += A(i, k) * x[k];
       NOC_UNROLL for (int j = 0; j < NU; ++j) t += Bm(i, j) * u[j];
       xn[i] = t;
@@ -558,7 +614,10 @@ static hipError_t launch_kkt(const KKTArgs& a, hipStream_t stream) {
   const long long threads = (long long)a.B * L;
   const int block = 256;
   const unsigned grid = (unsigned)((threads + block - 1) / block);
-  hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF>), dim3(grid), dim3(block), 0, stream, a);
+  if (a.tiled)
+    hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true>), dim3(grid), dim3(block), 0, stream, a);
+  else
+    hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, false>), dim3(grid), dim3(block), 0, stream, a);
   return hipGetLastError();
 }
 

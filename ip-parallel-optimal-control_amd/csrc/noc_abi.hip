@@ -70,7 +70,7 @@ const char* noc_last_error(void) { return g_last_error.c_str(); }
 int noc_kkt_supported(int nx, int nu) { return noc::kkt_supported(nx, nu) ? 1 : 0; }
 int noc_kkt_default_lanes(int nx, int nu, int N) { return noc::kkt_default_lanes(nx, nu, N); }
 
-static int kkt_common(int mode, int nx, int nu, int N, int B, int lanes, const double* A,
+static int kkt_common(int mode, int tiled, int nx, int nu, int N, int B, int lanes, const double* A,
                       const double* Bm, const double* Q, const double* R, const double* M,
                       const double* r, const double* q, const double* c, const double* P,
                       const double* p, const double* x0, const double* reg, const int* active,
@@ -108,6 +108,8 @@ static int kkt_common(int mode, int nx, int nu, int N, int B, int lanes, const d
   a.dx = dx; a.du = du; a.pred = pred; a.K = K; a.d = d; a.S = S; a.v = v;
   a.feasible = feasible;
   a.ablate = g_ablate;
+  a.tiled = tiled;
+  if (tiled && lanes == 0) return fail(-1, "the tiled layout needs an explicit lanes value");
   (void)bwd;
   (void)fwd;
   const int L = lanes ? lanes : noc::kkt_default_lanes(nx, nu, N);
@@ -121,8 +123,35 @@ int noc_kkt_solve(int nx, int nu, int N, int B, int lanes, const double* A, cons
                   const double* x0, const double* reg, const int* active, double* dx, double* du,
                   double* pred, int* feasible, double* K, double* d, double* S, double* v,
                   void* stream) {
-  return kkt_common(noc::MODE_FULL, nx, nu, N, B, lanes, A, Bm, Q, R, M, r, q, c, P, p, x0, reg,
+  return kkt_common(noc::MODE_FULL, 0, nx, nu, N, B, lanes, A, Bm, Q, R, M, r, q, c, P, p, x0, reg,
                     active, dx, du, pred, feasible, K, d, S, v, stream);
+}
+
+int noc_kkt_solve_tiled(int nx, int nu, int N, int B, int lanes, const double* A,
+                        const double* Bm, const double* Q, const double* R, const double* M,
+                        const double* r, const double* q, const double* c, const double* P,
+                        const double* p, const double* x0, const double* reg, const int* active,
+                        double* dx, double* du, double* pred, int* feasible, double* K, double* d,
+                        double* S, double* v, void* stream) {
+  return kkt_common(noc::MODE_FULL, 1, nx, nu, N, B, lanes, A, Bm, Q, R, M, r, q, c, P, p, x0,
+                    reg, active, dx, du, pred, feasible, K, d, S, v, stream);
+}
+
+long long noc_tiled_doubles(int N, int B, int lanes, int E) {
+  if (N < 1 || B < 0 || lanes < 1 || E < 1) return -1;
+  const long long cmax = (N + lanes - 1) / lanes;
+  return (long long)B * cmax * E * lanes;
+}
+
+int noc_relayout(int direction, int E, int sym_n, int N, int B, int lanes, const double* src,
+                 double* dst, void* stream) {
+  if (direction != 0 && direction != 1) return fail(-1, "direction must be 0 or 1");
+  if (N < 1 || B < 0 || E < 1) return fail(-1, "bad dims");
+  if (lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64) return fail(-1, "lanes must be 8/16/32/64");
+  if (sym_n > 0 && E != sym_n * (sym_n + 1) / 2) return fail(-1, "E must be sym_n(sym_n+1)/2");
+  if (!src || !dst) return fail(-2, "NULL pointer");
+  return hip_status(noc::relayout(direction, E, sym_n, N, B, lanes, src, dst,
+                                  static_cast<hipStream_t>(stream)), "relayout");
 }
 
 int noc_par_bwd_pass(int nx, int nu, int N, int B, int lanes, const double* A, const double* Bm,
@@ -130,14 +159,14 @@ int noc_par_bwd_pass(int nx, int nu, int N, int B, int lanes, const double* A, c
                      const double* q, const double* c, const double* P, const double* p,
                      const double* reg, const int* active, double* K, double* d, double* S,
                      double* v, double* pred, int* feasible, void* stream) {
-  return kkt_common(noc::MODE_BWD, nx, nu, N, B, lanes, A, Bm, Q, R, M, r, q, c, P, p, nullptr,
+  return kkt_common(noc::MODE_BWD, 0, nx, nu, N, B, lanes, A, Bm, Q, R, M, r, q, c, P, p, nullptr,
                     reg, active, nullptr, nullptr, pred, feasible, K, d, S, v, stream);
 }
 
 int noc_par_fwd_pass(int nx, int nu, int N, int B, int lanes, const double* A, const double* Bm,
                      const double* c, const double* x0, const double* K, const double* d,
                      const int* active, double* du, double* dx, void* stream) {
-  return kkt_common(noc::MODE_FWD, nx, nu, N, B, lanes, A, Bm, nullptr, nullptr, nullptr,
+  return kkt_common(noc::MODE_FWD, 0, nx, nu, N, B, lanes, A, Bm, nullptr, nullptr, nullptr,
                     nullptr, nullptr, c, nullptr, nullptr, x0, nullptr, active, dx, du, nullptr,
                     nullptr, const_cast<double*>(K), const_cast<double*>(d), nullptr, nullptr,
                     stream);
@@ -150,6 +179,8 @@ int noc_family_supported(const noc_family* fam) {
 static int check_ipm(const noc_family* fam, const noc_ipm_ws* ws) {
   if (!ws) return fail(-2, "workspace is NULL");
   if (ws->Bt < 0 || ws->N < 1) return fail(-1, "workspace dims: need Bt >= 0, N >= 1");
+  if (ws->lanes != 8 && ws->lanes != 16 && ws->lanes != 32 && ws->lanes != 64)
+    return fail(-1, "workspace lanes must be 8, 16, 32 or 64");
   if (fam && !noc::family_supported(*fam))
     return fail(-1, "unsupported problem family (kind/nx/nu)");
   const void* req[] = {ws->x, ws->u, ws->x0, ws->A, ws->B, ws->Q, ws->R, ws->M, ws->r, ws->P,
@@ -195,7 +226,8 @@ int noc_ipm_step(const noc_family* fam, const noc_ipm_ws* ws, int mode, int term
                  void* stream) {
   int rc = noc_ipm_prepare(fam, ws, mode, terminal, stream);
   if (rc) return rc;
-  rc = noc_kkt_solve(fam->nx, fam->nu, ws->N, ws->Bt, lanes, ws->A, ws->B, ws->Q, ws->R, ws->M,
+  (void)lanes;  // the KKT scan must use the workspace's tiled lane count
+  rc = noc_kkt_solve_tiled(fam->nx, fam->nu, ws->N, ws->Bt, ws->lanes, ws->A, ws->B, ws->Q, ws->R, ws->M,
                      ws->r, nullptr, nullptr, ws->P, nullptr, nullptr, ws->reg, ws->kkt_active,
                      ws->dx, ws->du, ws->pred, ws->feasible, ws->K, ws->d, nullptr, nullptr,
                      stream);

@@ -16,6 +16,7 @@ struct KKTArgs {
   double *dx, *du, *pred, *K, *d, *S, *v;
   int* feasible;
   int ablate;  // timing-only ablation bits (tools/kkt_ablate.py); 0 in every product call
+  int tiled;   // 1: A, B, Q, R, M, r, q, c, K, d in the tiled layout (Q, R packed symmetric)
 };
 
 hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t stream);
@@ -29,6 +30,8 @@ hipError_t ipm_prepare(const noc_family& p, const noc_ipm_ws& w, int mode, int t
                        hipStream_t s);
 hipError_t ipm_trial(const noc_family& p, const noc_ipm_ws& w, int mode, hipStream_t s);
 hipError_t ipm_init(const noc_ipm_ws& w, double bp0, hipStream_t s);
+hipError_t relayout(int direction, int E, int sym_n, int N, int Bt, int L, const double* src,
+                    double* dst, hipStream_t s);
 bool family_supported(const noc_family& p);
 
 }  // namespace noc

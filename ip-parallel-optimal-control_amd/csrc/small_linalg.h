@@ -90,6 +90,82 @@ NOC_DEV void gstore_sym(double* __restrict__ dst, const Sym<N>& S) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Tiled ("lane-interleaved") block layout, see include/noc_hip.h.  A field with E doubles per
+// stage, trajectory segments of L lanes and cmax = ceil(N/L) chunk slots: stage s owned by lane l
+// at chunk position j lives at
+//   E even: (((traj*cmax + j)*(E/2) + e/2)*L + l)*2 + (e&1)     (16-byte granules)
+//   E odd : ((traj*cmax + j)*E + e)*L + l                         (8-byte granules)
+// so one wave-wide load of a granule is L*16 (L*8) contiguous bytes.
+template <int E, int L>
+NOC_DEV size_t tile_base(int traj, int j, int l, int cmax) {
+  if constexpr (E % 2 == 0) return (((size_t)traj * cmax + j) * (E / 2) * L + l) * 2;
+  else return ((size_t)traj * cmax + j) * E * L + l;
+}
+template <int E, int L>
+NOC_DEV void tload(const double* __restrict__ base, int traj, int j, int l, int cmax, double* dst) {
+  const double* p = base + tile_base<E, L>(traj, j, l, cmax);
+  if constexpr (E % 2 == 0) {
+    NOC_UNROLL for (int q = 0; q < E / 2; ++q) {
+      const double2 v = *reinterpret_cast<const double2*>(p + (size_t)q * 2 * L);
+      dst[2 * q] = v.x;
+      dst[2 * q + 1] = v.y;
+    }
+  } else {
+    NOC_UNROLL for (int e = 0; e < E; ++e) dst[e] = p[(size_t)e * L];
+  }
+}
+template <int E, int L>
+NOC_DEV void tstore(double* __restrict__ base, int traj, int j, int l, int cmax, const double* src) {
+  double* p = base + tile_base<E, L>(traj, j, l, cmax);
+  if constexpr (E % 2 == 0) {
+    NOC_UNROLL for (int q = 0; q < E / 2; ++q)
+      *reinterpret_cast<double2*>(p + (size_t)q * 2 * L) = make_double2(src[2 * q], src[2 * q + 1]);
+  } else {
+    NOC_UNROLL for (int e = 0; e < E; ++e) p[(size_t)e * L] = src[e];
+  }
+}
+// runtime-E variant (relayout / linearisation kernels)
+NOC_DEV size_t tile_index(int E, int L, int cmax, int traj, int j, int l, int e) {
+  if ((E & 1) == 0) return (((size_t)traj * cmax + j) * (E / 2) + (e >> 1)) * (2 * L) + 2 * l + (e & 1);
+  return (((size_t)traj * cmax + j) * E + e) * L + l;
+}
+template <int E>
+NOC_DEV void tload_rt(const double* __restrict__ base, int L, int cmax, int traj, int j, int l, double* dst) {
+  const double* p = base + tile_index(E, L, cmax, traj, j, l, 0);
+  if constexpr (E % 2 == 0) {
+    NOC_UNROLL for (int q = 0; q < E / 2; ++q) {
+      const double2 v = *reinterpret_cast<const double2*>(p + (size_t)q * 2 * L);
+      dst[2 * q] = v.x;
+      dst[2 * q + 1] = v.y;
+    }
+  } else {
+    NOC_UNROLL for (int e = 0; e < E; ++e) dst[e] = p[(size_t)e * L];
+  }
+}
+template <int E>
+NOC_DEV void tstore_rt(double* __restrict__ base, int L, int cmax, int traj, int j, int l, const double* src) {
+  double* p = base + tile_index(E, L, cmax, traj, j, l, 0);
+  if constexpr (E % 2 == 0) {
+    NOC_UNROLL for (int q = 0; q < E / 2; ++q)
+      *reinterpret_cast<double2*>(p + (size_t)q * 2 * L) = make_double2(src[2 * q], src[2 * q + 1]);
+  } else {
+    NOC_UNROLL for (int e = 0; e < E; ++e) p[(size_t)e * L] = src[e];
+  }
+}
+// chunk geometry of a horizon N split over L lanes (lanes < rem get one extra stage)
+struct Chunks {
+  int base, rem, cmax;
+  NOC_DEV Chunks(int N, int L) : base(N / L), rem(N % L), cmax(N / L + (N % L ? 1 : 0)) {}
+  NOC_DEV int start(int l) const { return l * base + (l < rem ? l : rem); }
+  NOC_DEV int len(int l) const { return base + (l < rem ? 1 : 0); }
+  NOC_DEV void owner(int s, int& l, int& j) const {  // stage -> (lane, chunk position)
+    const int cut = rem * (base + 1);
+    if (s < cut) { l = s / (base + 1); j = s - l * (base + 1); }
+    else { l = rem + (s - cut) / base; j = (s - cut) - (l - rem) * base; }
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
 // wave shuffles of whole register blocks (ds_bpermute under the hood, segment width W)
 NOC_DEV double shfl_down_d(double x, int d, int w) { return __shfl_down(x, (unsigned)d, w); }
 NOC_DEV double shfl_up_d(double x, int d, int w) { return __shfl_up(x, (unsigned)d, w); }
@@ -141,6 +217,36 @@ NOC_DEV bool ldl_solve(const Sym<N>& W, double (&Y)[N][NR]) {
         NOC_UNROLL for (int j = 0; j < NR; ++j) Y[i][j] -= Lm[t][i] * Y[t][j];
     return pd;
   }
+}
+
+// Gaussian elimination WITHOUT row exchanges, accepted only if every pivot passes the
+// threshold-pivoting test |p_k| >= tau * max_{i>=k} |x_ik| (tau = 1/2 bounds element growth like
+// partial pivoting does, within a factor (1+1/tau)^(N-1)).  Returns false (X, Y garbage) if a
+// pivot fails; the caller then redoes the solve with lu_pp_solve.  No selects: ~1/3 fewer VALU
+// instructions than the pivoting solve.
+template <int N, int NR>
+NOC_DEV bool lu_np_solve(double (&X)[N][N], double (&Y)[N][NR]) {
+  bool ok = true;
+  NOC_UNROLL for (int k = 0; k < N; ++k) {
+    double colmax = fabs(X[k][k]);
+    NOC_UNROLL for (int i = k + 1; i < N; ++i) colmax = fmax(colmax, fabs(X[i][k]));
+    ok = ok && (fabs(X[k][k]) >= 0.5 * colmax) && (colmax > 0.0);
+    const double inv = 1.0 / X[k][k];
+    X[k][k] = inv;
+    NOC_UNROLL for (int i = k + 1; i < N; ++i) {
+      const double lik = X[i][k] * inv;
+      NOC_UNROLL for (int j = k + 1; j < N; ++j) X[i][j] -= lik * X[k][j];
+      NOC_UNROLL for (int j = 0; j < NR; ++j) Y[i][j] -= lik * Y[k][j];
+    }
+  }
+  NOC_UNROLL for (int k = N - 1; k >= 0; --k) {
+    NOC_UNROLL for (int j = 0; j < NR; ++j) {
+      double s = Y[k][j];
+      NOC_UNROLL for (int t = k + 1; t < N; ++t) s -= X[k][t] * Y[t][j];
+      Y[k][j] = s * X[k][k];
+    }
+  }
+  return ok;
 }
 
 // Gaussian elimination with partial pivoting (row swaps as selects, so everything stays in

@@ -24,6 +24,9 @@ SIGNATURES = {
     "noc_kkt_default_lanes": (_i, [_i, _i, _i]),
     "noc_debug_set_ablation": (None, [_i]),
     "noc_kkt_solve": (_i, [_i] * 5 + [_dp] * 13 + [_dp] * 8 + [_dp]),
+    "noc_kkt_solve_tiled": (_i, [_i] * 5 + [_dp] * 13 + [_dp] * 8 + [_dp]),
+    "noc_tiled_doubles": (ctypes.c_longlong, [_i, _i, _i, _i]),
+    "noc_relayout": (_i, [_i] * 6 + [_dp, _dp, _dp]),
     "noc_par_bwd_pass": (_i, [_i] * 5 + [_dp] * 12 + [_dp] * 6 + [_dp]),
     "noc_par_fwd_pass": (_i, [_i] * 5 + [_dp] * 7 + [_dp] * 2 + [_dp]),
 }
@@ -50,7 +53,8 @@ WS_STATE_FIELDS = ["bp", "rp", "rinc", "cost", "hu", "gnorm", "reg"]
 
 
 class NocIpmWs(ctypes.Structure):
-    _fields_ = ([("Bt", _i), ("N", _i)] + [(f, _dp) for f in WS_DOUBLE_FIELDS]
+    _fields_ = ([("Bt", _i), ("N", _i), ("lanes", _i), ("reserved", _i)]
+                + [(f, _dp) for f in WS_DOUBLE_FIELDS]
                 + [(f, _dp) for f in WS_INT_FIELDS] + [(f, _dp) for f in WS_STATE_FIELDS])
 
 

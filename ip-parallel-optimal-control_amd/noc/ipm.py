@@ -27,25 +27,28 @@ class BatchedIPM:
         self.N, self.Bt = int(N), int(batch)
         self.nx, self.nu = family.nx, family.nu
         self.device = torch.device(device)
-        self.lanes = lanes
         lib = _lib.load()
+        self.lanes = lanes or lib.noc_kkt_default_lanes(family.nx, family.nu, N)
         if not lib.noc_family_supported(ctypes.byref(self.fam_c)):
             raise _lib.NocError(f"unsupported family kind={family.kind} nx={family.nx} nu={family.nu}")
         Bt, N, nx, nu = self.Bt, self.N, self.nx, self.nu
         f64 = dict(device=self.device, dtype=torch.float64)
         i32 = dict(device=self.device, dtype=torch.int32)
-        shapes = dict(x=(Bt, N + 1, nx), u=(Bt, N, nu), x0=(Bt, nx), A=(Bt, N, nx, nx),
-                      B=(Bt, N, nx, nu), Q=(Bt, N, nx, nx), R=(Bt, N, nu, nu), M=(Bt, N, nx, nu),
-                      r=(Bt, N, nu), P=(Bt, nx, nx), cx=(Bt, N, nx), cu=(Bt, N, nu), lc=(Bt, N),
-                      lam=(Bt, N + 1, nx), dx=(Bt, N + 1, nx), du=(Bt, N, nu), pred=(Bt,),
-                      K=(Bt, N, nu, nx), d=(Bt, N, nu))
+        L = self.lanes
+        tiled = lambda E: (int(lib.noc_tiled_doubles(N, Bt, L, E)),)
+        # LQ blocks and gains in the KKT scan's tiled layout (Q, R packed symmetric)
+        shapes = dict(x=(Bt, N + 1, nx), u=(Bt, N, nu), x0=(Bt, nx), A=tiled(nx * nx),
+                      B=tiled(nx * nu), Q=tiled(nx * (nx + 1) // 2), R=tiled(nu * (nu + 1) // 2),
+                      M=tiled(nx * nu), r=tiled(nu), P=(Bt, nx, nx), cx=(Bt, N, nx),
+                      cu=(Bt, N, nu), lc=(Bt, N), lam=(Bt, N + 1, nx), dx=(Bt, N + 1, nx),
+                      du=(Bt, N, nu), pred=(Bt,), K=tiled(nu * nx), d=tiled(nu))
         self.t = {k: torch.zeros(s, **f64) for k, s in shapes.items()}
         for k in _lib.WS_INT_FIELDS:
             self.t[k] = torch.zeros(Bt, **i32)
         for k in _lib.WS_STATE_FIELDS:
             self.t[k] = torch.zeros(Bt, **f64)
         ws = _lib.NocIpmWs()
-        ws.Bt, ws.N = Bt, N
+        ws.Bt, ws.N, ws.lanes = Bt, N, L
         for k in _lib.WS_DOUBLE_FIELDS + _lib.WS_INT_FIELDS + _lib.WS_STATE_FIELDS:
             setattr(ws, k, self.t[k].data_ptr())
         self.ws = ws
@@ -93,6 +96,22 @@ class BatchedIPM:
             if self.all_done():
                 break
         return steps
+
+    def tiled_blocks(self):
+        from .lqt import TiledBlocks
+        t = self.t
+        return TiledBlocks(t["A"], t["B"], t["Q"], t["R"], t["M"], t["r"], t["P"], self.nx,
+                           self.nu, self.N, self.Bt, self.lanes)
+
+    def natural_blocks(self):
+        """The LQ blocks relaid out to the natural (Bt, N, ...) layout (tests / export)."""
+        from .lqt import untile
+        Bt, N, nx, nu, L, t = self.Bt, self.N, self.nx, self.nu, self.lanes, self.t
+        return dict(A=untile(t["A"], (Bt, N, nx, nx), L), B=untile(t["B"], (Bt, N, nx, nu), L),
+                    Q=untile(t["Q"], (Bt, N, nx, nx), L, sym=True),
+                    R=untile(t["R"], (Bt, N, nu, nu), L, sym=True),
+                    M=untile(t["M"], (Bt, N, nx, nu), L), r=untile(t["r"], (Bt, N, nu), L),
+                    P=t["P"])
 
     # -------------------------------------------------------------------------------------------
     def result(self):

@@ -86,6 +86,95 @@ def kkt_solve(A, B, Q, R, M, r, P, reg=None, x0=None, q=None, c=None, p=None, ac
     return out
 
 
+# ------------------------------------------------------------------------------------------------
+# tiled ("lane-interleaved") layout: the KKT scan's native HBM layout (include/noc_hip.h)
+# ------------------------------------------------------------------------------------------------
+def tiled_numel(N: int, Bt: int, lanes: int, E: int) -> int:
+    return int(_lib.load().noc_tiled_doubles(N, Bt, lanes, E))
+
+
+def tile(t: torch.Tensor, lanes: int, sym: bool = False) -> torch.Tensor:
+    """Natural (Bt, N, ...) field -> flat tiled buffer.  sym=True packs an (n x n) symmetric
+    field (upper triangle)."""
+    t = _c(t, "field")
+    Bt, N = t.shape[0], t.shape[1]
+    if sym:
+        n = t.shape[-1]
+        E, sym_n = n * (n + 1) // 2, n
+    else:
+        E, sym_n = int(t[0, 0].numel()), 0
+    out = torch.empty(tiled_numel(N, Bt, lanes, E), dtype=torch.float64, device=t.device)
+    _lib.check(_lib.load().noc_relayout(0, E, sym_n, N, Bt, lanes, t.data_ptr(), out.data_ptr(),
+                                        _lib.stream_handle(t.device)), "noc_relayout")
+    return out
+
+
+def untile(buf: torch.Tensor, shape, lanes: int, sym: bool = False) -> torch.Tensor:
+    """Inverse of `tile`: flat tiled buffer -> natural tensor of `shape` = (Bt, N, ...)."""
+    Bt, N = shape[0], shape[1]
+    if sym:
+        n = shape[-1]
+        E, sym_n = n * (n + 1) // 2, n
+    else:
+        E = 1
+        for d in shape[2:]:
+            E *= d
+        sym_n = 0
+    out = torch.empty(shape, dtype=torch.float64, device=buf.device)
+    _lib.check(_lib.load().noc_relayout(1, E, sym_n, N, Bt, lanes, buf.data_ptr(), out.data_ptr(),
+                                        _lib.stream_handle(buf.device)), "noc_relayout")
+    return out
+
+
+class TiledBlocks(NamedTuple):
+    """LQ blocks of Bt trajectories x N stages in the tiled layout of `lanes`."""
+    A: torch.Tensor
+    B: torch.Tensor
+    Q: torch.Tensor        # packed symmetric
+    R: torch.Tensor        # packed symmetric
+    M: torch.Tensor
+    r: torch.Tensor
+    P: torch.Tensor        # natural (Bt, nx, nx)
+    nx: int
+    nu: int
+    N: int
+    Bt: int
+    lanes: int
+
+
+def to_tiled(A, B, Q, R, M, r, P, lanes: int) -> TiledBlocks:
+    Bt, N, nx, _ = A.shape
+    nu = B.shape[-1]
+    return TiledBlocks(tile(A, lanes), tile(B, lanes), tile(Q, lanes, sym=True),
+                       tile(R, lanes, sym=True), tile(M, lanes), tile(r, lanes), _c(P, "P"),
+                       nx, nu, N, Bt, lanes)
+
+
+def kkt_solve_tiled(tb: TiledBlocks, reg=None, x0=None, active=None, want_value=False,
+                    out: Optional[KKTResult] = None) -> KKTResult:
+    """Fused KKT solve on tiled blocks (the layout the interior-point workspace produces).
+    K, d of the result are flat tiled buffers; dx, du, S, v natural."""
+    Bt, N, nx, nu, L = tb.Bt, tb.N, tb.nx, tb.nu, tb.lanes
+    dev = tb.A.device
+    if out is None:
+        f64 = dict(device=dev, dtype=torch.float64)
+        out = KKTResult(
+            torch.empty(Bt, N + 1, nx, **f64), torch.empty(Bt, N, nu, **f64),
+            torch.empty(Bt, **f64), torch.empty(Bt, device=dev, dtype=torch.int32),
+            torch.empty(tiled_numel(N, Bt, L, nu * nx), **f64),
+            torch.empty(tiled_numel(N, Bt, L, nu), **f64),
+            torch.empty(Bt, N + 1, nx, nx, **f64) if want_value else None,
+            torch.empty(Bt, N + 1, nx, **f64) if want_value else None)
+    if active is not None:
+        active = active.to(device=dev, dtype=torch.int32).contiguous()
+    rc = _lib.load().noc_kkt_solve_tiled(nx, nu, N, Bt, L, *(_lib.ptr(t) for t in (
+        tb.A, tb.B, tb.Q, tb.R, tb.M, tb.r, None, None, tb.P, None, _c(x0, "x0"), _c(reg, "reg"),
+        active, out.dx, out.du, out.pred, out.feasible, out.K, out.d, out.S, out.v)),
+        _lib.stream_handle(dev))
+    _lib.check(rc, "noc_kkt_solve_tiled")
+    return out
+
+
 def bwd_pass(A, B, Q, R, M, r, P, reg=None, q=None, c=None, p=None, active=None, lanes=0):
     """Backward pass only -> (K, d, S, v, pred, feasible) (paroc.par_bwd_pass semantics)."""
     squeeze, (A, B, Q, R, M, r, P, q, c, p) = _batched(A, B, Q, R, M, r, P, q, c, p)

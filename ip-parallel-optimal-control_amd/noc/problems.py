@@ -182,17 +182,21 @@ def make_problem(name: str, N: int) -> OCP:
     raise ValueError(name)
 
 
-def make_bench_blocks(name: str, N: int, batch: int, seed: int = 0, device="cuda"):
+def make_bench_blocks(name: str, N: int, batch: int, seed: int = 0, device="cuda", lanes: int = 0,
+                      natural: bool = False):
     """Realistic LQ blocks of the first Newton step (bp = 0.1, rp = 1) of `batch` trajectories,
-    produced on the GPU by the HIP linearisation kernels.  Returns a dict of CUDA tensors with the
-    noc_kkt_solve layouts (A, B, Q, R, M, r, P, reg, x, u)."""
+    produced on the GPU by the HIP linearisation kernels, in the KKT scan's tiled layout
+    (`tiled`: noc.lqt.TiledBlocks).  natural=True also returns the natural-layout copies
+    (A, B, Q, R, M, r, P) for checks.  `reg`, `x`, `u` are natural."""
     from .ipm import BatchedIPM
     ocp = make_problem(name, N)
     x0, u0 = initial_conditions(name, N, batch, seed)
-    eng = BatchedIPM(ocp.family, N, batch, device=device)
+    eng = BatchedIPM(ocp.family, N, batch, device=device, lanes=lanes)
     eng.load(u0, x0)
     eng.init(bp0=0.1)
     eng.prepare(mode=_lib.MODE_PAR, terminal=_lib.TERMINAL_FINAL_COST)
     t = eng.t
-    return dict(A=t["A"], B=t["B"], Q=t["Q"], R=t["R"], M=t["M"], r=t["r"], P=t["P"],
-                reg=t["reg"], x=t["x"], u=t["u"], engine=eng)
+    out = dict(tiled=eng.tiled_blocks(), reg=t["reg"], x=t["x"], u=t["u"], engine=eng)
+    if natural:
+        out.update(eng.natural_blocks())
+    return out

@@ -32,7 +32,7 @@ def _oracle_problem(name, N):
 def test_device_linearisation_matches_autodiff_oracle(name, N):
     from noc.problems import make_bench_blocks
     from oracle import noc_oracle as O
-    blk = make_bench_blocks(name, N=N, batch=3, seed=5)
+    blk = make_bench_blocks(name, N=N, batch=3, seed=5, natural=True)
     torch.cuda.synchronize()
     prob = _oracle_problem(name, N)
     X = blk["x"].cpu().numpy()

@@ -136,21 +136,58 @@ def test_lqt_tracking_form_adapter():
     assert bool(feas)
 
 
+@pytest.mark.parametrize("nx,nu", [(2, 1), (4, 1), (8, 4)])
+@pytest.mark.parametrize("lanes", [64, 32, 16, 8])
+@pytest.mark.parametrize("N", [1, 13, 200])
+def test_tiled_layout_kkt_matches_oracle(nx, nu, lanes, N):
+    """The tiled (lane-interleaved, Q/R packed) layout the IPM workspace uses."""
+    from noc import lqt
+    case = rand_lq(77 * nx + N + lanes, 5, N, nx, nu)
+    ref = oracle_batch(case)
+    g = lambda k: dev(case[k])
+    tb = lqt.to_tiled(g("A"), g("B"), g("Q"), g("R"), g("M"), g("r"), g("P"), lanes)
+    out = lqt.kkt_solve_tiled(tb, reg=g("reg"), want_value=True)
+    torch.cuda.synchronize()
+    for k in ["dx", "du", "S", "v", "pred"]:
+        assert relerr(getattr(out, k).cpu(), ref[k]) < RTOL, k
+    K = lqt.untile(out.K, (5, N, nu, nx), lanes)
+    d = lqt.untile(out.d, (5, N, nu), lanes)
+    assert relerr(K.cpu(), ref["K"]) < RTOL and relerr(d.cpu(), ref["d"]) < RTOL
+    assert np.array_equal(out.feasible.cpu().numpy().astype(bool), ref["feasible"].astype(bool))
+
+
+@pytest.mark.parametrize("lanes", [64, 16])
+def test_tile_untile_roundtrip(lanes):
+    from noc import lqt
+    rng = np.random.default_rng(0)
+    for shape, sym in [((3, 37, 4, 4), False), ((3, 37, 4, 1), False), ((3, 37, 1), False),
+                       ((3, 37, 8, 8), True), ((2, 5, 2, 2), True)]:
+        x = rng.normal(size=shape)
+        if sym:
+            x = x + np.swapaxes(x, -1, -2)
+        t = dev(x)
+        back = lqt.untile(lqt.tile(t, lanes, sym=sym), shape, lanes, sym=sym)
+        assert torch.equal(back.cpu(), torch.as_tensor(x))
+
+
 def test_cartpole_blocks_full_size_properties():
-    """BASELINE config c3 size (N=200, B=4096): realistic cart-pole Newton blocks.
-    Checks (size-independent): dynamics consistency dx_{k+1} = A dx_k + B du_k exactly (to
-    rounding), oracle parity on a strided sample of 16 trajectories, all feasible."""
+    """BASELINE config c3 size (N=200, B=4096): realistic cart-pole Newton blocks produced by the
+    device linearisation in the tiled layout.  Checks (size-independent): dynamics consistency
+    dx_{k+1} = A dx_k + B du_k on all trajectories, oracle parity on a strided sample of 16
+    trajectories, all feasible, and tiled == natural-layout solve."""
     from noc import lqt
     from noc.problems import make_bench_blocks
-    blocks = make_bench_blocks("cartpole", N=200, batch=4096, seed=0)
-    res = lqt.kkt_solve(blocks["A"], blocks["B"], blocks["Q"], blocks["R"], blocks["M"],
-                        blocks["r"], blocks["P"], reg=blocks["reg"])
+    blocks = make_bench_blocks("cartpole", N=200, batch=4096, seed=0, natural=True)
+    res = lqt.kkt_solve_tiled(blocks["tiled"], reg=blocks["reg"])
+    nat = lqt.kkt_solve(blocks["A"], blocks["B"], blocks["Q"], blocks["R"], blocks["M"],
+                        blocks["r"], blocks["P"], reg=blocks["reg"], lanes=64)
     torch.cuda.synchronize()
     dx, du = res.dx, res.du
     pred_dx = torch.einsum("bkij,bkj->bki", blocks["A"], dx[:, :-1]) + \
         torch.einsum("bkij,bkj->bki", blocks["B"], du)
     scale = dx.abs().max().item()
     assert (pred_dx - dx[:, 1:]).abs().max().item() <= 1e-12 * max(1.0, scale)
+    assert (nat.dx - dx).abs().max().item() <= 1e-12 * max(1.0, scale)
     sample = list(range(0, 4096, 256))
     case = {k: blocks[k][sample].cpu().numpy() for k in ["A", "B", "Q", "R", "M", "r", "P", "reg"]}
     ref = oracle_batch(case)

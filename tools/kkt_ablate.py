@@ -9,9 +9,10 @@ from noc import lqt, problems, _lib
 
 name, N, B = (sys.argv[1], int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else ("cartpole", 200, 4096)
 lanes = int(sys.argv[4]) if len(sys.argv) > 4 else 64
-blk = problems.make_bench_blocks(name, N=N, batch=B, seed=7)
+blk = problems.make_bench_blocks(name, N=N, batch=B, seed=7, lanes=lanes)
+tb = blk["tiled"]
 lib = _lib.load()
-out = lqt.kkt_solve(blk["A"], blk["B"], blk["Q"], blk["R"], blk["M"], blk["r"], blk["P"], reg=blk["reg"], lanes=lanes)
+out = lqt.kkt_solve_tiled(tb, reg=blk["reg"])
 variants = {"full": 0, "no_fwd": 2, "no_scan": 1, "no_scan_no_fwd": 3, "phase1_only": 5, "phase1+2": 4}
 times = {k: [] for k in variants}
 for _ in range(5):
@@ -20,7 +21,7 @@ for _ in range(5):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(10):
-            lqt.kkt_solve(blk["A"], blk["B"], blk["Q"], blk["R"], blk["M"], blk["r"], blk["P"], reg=blk["reg"], lanes=lanes, out=out)
+            lqt.kkt_solve_tiled(tb, reg=blk["reg"], out=out)
         e1.record(); torch.cuda.synchronize()
         times[k].append(e0.elapsed_time(e1) / 10)
 lib.noc_debug_set_ablation(0)
