@@ -273,9 +273,13 @@ NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
       J2A1(i, j) = s;
     }
   }
-  // Y = [TA | Tb | TC],  T = (I + C1 J2)^-1: threshold-checked solve without row exchanges,
-  // partial pivoting for the (rare) lanes whose check fails
-  if (!lu_np_solve<NX, NR>(X, Y)) {
+  // Y = [TA | Tb | TC],  T = (I + C1 J2)^-1: threshold-checked solve without row exchanges; if
+  // any lane's check fails the whole wave (uniform branch, so the re-shuffle is legal) redoes
+  // the solve with partial pivoting.  J2 / nu2 are re-fetched there instead of kept live.
+  const bool ok = lu_np_solve<NX, NR>(X, Y);
+  if (__any(!ok)) {
+    shfl_down_arr<Sym<NX>::SZ>(e1.J.v, J2.v, d, L);
+    shfl_down_arr<NX>(e1.nu.v, nu2.v, d, L);
     build();
     lu_pp_solve<NX, NR>(X, Y);
   }
@@ -328,7 +332,7 @@ NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
 }
 
 template <int NX, int NU, int L, bool AFF, bool TILED>
-__global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
+__global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int traj = tid / L;
   const int l = tid % L;
@@ -581,21 +585,45 @@ __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(K
   Vec<NX> x;
   shfl_up_arr<NX>(phi.v, x.v, 1, L);
   if (l == 0) x = x0;
+  // dx/du rows go through LDS (one region per trajectory segment) and leave as whole contiguous
+  // rows: per-lane direct stores would touch one cache line per lane per store instruction.
+  extern __shared__ __attribute__((aligned(16))) double noc_smem[];
+  const int rows_dx = (N + 1) * NX, rows_du = N * NU;
+  const int per_traj = (rows_dx + rows_du + 1) & ~1;
+  double* sdx = noc_smem + (size_t)(threadIdx.x / L) * per_traj;
+  double* sdu = sdx + rows_dx;
+  const bool via_lds = a.lds_out != 0;
+  Mat<NX, NX> nA;
+  Mat<NX, NU> nB;
+  double nK[NU * (NX + 1)];
+  Vec<NX> nc;
+  if (len > 0) {
+    load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + start, 0, l, cmax, nA, nB, nc);
+    load_Kd<NX, NU, L, TILED>(a, traj, tN + start, 0, l, cmax, nK);
+  }
   for (int s = start; s < start + len; ++s) {
-    Mat<NX, NX> A;
-    Mat<NX, NU> Bm;
+    const Mat<NX, NX> A = nA;
+    const Mat<NX, NU> Bm = nB;
+    const Vec<NX> cc = nc;
     double Kk[NU * (NX + 1)];
-    Vec<NX> cc;
-    load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + s, s - start, l, cmax, A, Bm, cc);
-    load_Kd<NX, NU, L, TILED>(a, traj, tN + s, s - start, l, cmax, Kk);
+    NOC_UNROLL for (int i = 0; i < NU * (NX + 1); ++i) Kk[i] = nK[i];
+    if (s + 1 < start + len) {  // prefetch the next stage
+      load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + s + 1, s + 1 - start, l, cmax, nA, nB, nc);
+      load_Kd<NX, NU, L, TILED>(a, traj, tN + s + 1, s + 1 - start, l, cmax, nK);
+    }
     Vec<NU> u;
     NOC_UNROLL for (int i = 0; i < NU; ++i) {
       double t = Kk[NU * NX + i];
       NOC_UNROLL for (int k = 0; k < NX; ++k) t += Kk[i * NX + k] * x[k];
       u[i] = t;
     }
-    if (a.dx) gstore<NX>(a.dx + (tN + traj + s) * NX, x.v);
-    if (a.du) gstore<NU>(a.du + (tN + s) * NU, u.v);
+    if (via_lds) {
+      NOC_UNROLL for (int i = 0; i < NX; ++i) sdx[s * NX + i] = x[i];
+      NOC_UNROLL for (int i = 0; i < NU; ++i) sdu[s * NU + i] = u[i];
+    } else {
+      if (a.dx) gstore<NX>(a.dx + (tN + traj + s) * NX, x.v);
+      if (a.du) gstore<NU>(a.du + (tN + s) * NU, u.v);
+    }
     Vec<NX> xn;
     NOC_UNROLL for (int i = 0; i < NX; ++i) {
       double t = cc[i];
@@ -605,19 +633,46 @@ __global__ __launch_bounds__(256, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(K
     }
     x = xn;
   }
-  if (last && a.dx) gstore<NX>(a.dx + (tN + traj + N) * NX, x.v);
+  if (!via_lds) {
+    if (last && a.dx) gstore<NX>(a.dx + (tN + traj + N) * NX, x.v);
+    return;
+  }
+  if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) sdx[N * NX + i] = x[i];
+  __syncthreads();  // one wave per block: orders this wave's LDS writes before its reads
+  if (a.dx) {
+    const double2* src = reinterpret_cast<const double2*>(sdx);
+    double2* dst = reinterpret_cast<double2*>(a.dx + (tN + traj) * NX);
+    if constexpr (NX % 2 == 0) {
+      for (int i = l; i < rows_dx / 2; i += L) dst[i] = src[i];
+    } else {
+      for (int i = l; i < rows_dx; i += L) a.dx[(tN + traj) * NX + i] = sdx[i];
+    }
+  }
+  if (a.du)
+    for (int i = l; i < rows_du; i += L) a.du[tN * NU + i] = sdu[i];
+}
+
+// dynamic LDS bytes of one 64-thread block when dx/du are staged (0: stage directly)
+template <int NX, int NU, int L>
+static size_t kkt_lds_bytes(int N) {
+  const size_t per_traj = (size_t)(((N + 1) * NX + N * NU + 1) & ~1);
+  const size_t bytes = (64 / L) * per_traj * sizeof(double);
+  return bytes <= 32768 ? bytes : 0;  // keep >= 4 blocks (waves) per CU resident
 }
 
 // ---------------------------------------------------------------------------------------------
 template <int NX, int NU, int L, bool AFF>
-static hipError_t launch_kkt(const KKTArgs& a, hipStream_t stream) {
+static hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
+  KKTArgs a = a_in;
   const long long threads = (long long)a.B * L;
-  const int block = 256;
+  const int block = 64;  // one wave per workgroup: waves are independent (no LDS sharing)
   const unsigned grid = (unsigned)((threads + block - 1) / block);
+  const size_t lds = (a.mode == MODE_BWD || (!a.dx && !a.du)) ? 0 : kkt_lds_bytes<NX, NU, L>(a.N);
+  a.lds_out = lds > 0 ? 1 : 0;
   if (a.tiled)
-    hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true>), dim3(grid), dim3(block), 0, stream, a);
+    hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true>), dim3(grid), dim3(block), lds, stream, a);
   else
-    hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, false>), dim3(grid), dim3(block), 0, stream, a);
+    hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, false>), dim3(grid), dim3(block), lds, stream, a);
   return hipGetLastError();
 }
 

@@ -54,11 +54,13 @@ hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t
   return hipErrorInvalidValue;
 }
 
+// lanes per trajectory chosen from the measured sweep (profiles/r01/kkt_lanes_sweep_tiled.log):
+// long horizons amortise the cross-lane scan over longer chunks (L = 32 at c3, N = 200); short
+// horizons need the lanes for parallelism (L = 64 at c2, N = 100).
 int kkt_default_lanes(int nx, int nu, int N) {
-  (void)nx;
   (void)nu;
-  (void)N;
-  return 64;
+  if (nx >= 8) return 16;
+  return N >= 160 ? 32 : 64;
 }
 }  // namespace noc
 

@@ -17,6 +17,7 @@ struct KKTArgs {
   int* feasible;
   int ablate;  // timing-only ablation bits (tools/kkt_ablate.py); 0 in every product call
   int tiled;   // 1: A, B, Q, R, M, r, q, c, K, d in the tiled layout (Q, R packed symmetric)
+  int lds_out; // set by the launcher: dx/du staged through LDS and written as contiguous rows
 };
 
 hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t stream);
