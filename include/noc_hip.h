@@ -108,6 +108,7 @@ int noc_par_fwd_pass(int nx, int nu, int N, int B, int lanes,
 #define NOC_PHASE_LINEARIZE 1
 #define NOC_PHASE_SOLVE 2
 #define NOC_PHASE_DONE 3
+#define NOC_PHASE_ROLLED 4 /* rolled out, waiting to be promoted to LINEARIZE (two-stream loop) */
 
 #define NOC_MODE_PAR 0 /* par_interior_point_newton semantics (retry loop, reg = rp*|cu|) */
 #define NOC_MODE_SEQ 1 /* seq_interior_point_newton semantics (one accept/reject, reg = mu) */
@@ -134,7 +135,7 @@ typedef struct noc_ipm_ws {
   int reserved;
   double *x, *u, *x0;                  /* (Bt,N+1,nx) (Bt,N,nu) (Bt,nx)           */
   double *A, *B, *Q, *R, *M, *r, *P;   /* LQ blocks: tiled (P natural)              */
-  double *cx, *cu, *lc, *lam;          /* (Bt,N,nx) (Bt,N,nu) (Bt,N) (Bt,N+1,nx)    */
+  double *cx, *cu, *lc, *lam;          /* cx, cu, lc tiled (E = nx, nu, 1); lam (Bt,N+1,nx) */
   double *dx, *du, *pred, *K, *d;      /* KKT outputs (dx, du natural; K, d tiled)  */
   int *feasible;                       /* (Bt) int32                               */
   int *phase, *kkt_active, *it, *inner, *total_it, *kkt_solves; /* (Bt) int32     */
@@ -149,9 +150,18 @@ int noc_ipm_prepare(const noc_family* fam, const noc_ipm_ws* ws, int mode, int t
                     void* stream);
 /* trial point, gain ratio, regularisation update, accept, stop test, barrier schedule. */
 int noc_ipm_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* stream);
-/* one device iteration: prepare + noc_kkt_solve(active = phase != DONE) + trial. */
+/* one device iteration: prepare + noc_kkt_solve(active = phase SOLVE) + trial. */
 int noc_ipm_step(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, int lanes,
                  void* stream);
+/* Two-stream form of one iteration (rollouts overlap the other trajectories' Newton step):
+ *   roll stream : wait(prev main event); noc_ipm_rollout      (ROLLOUT -> ROLLED)
+ *   main stream : noc_ipm_step_main (LINEARIZE..SOLVE..trial); wait(roll event);
+ *                 noc_ipm_promote                              (ROLLED  -> LINEARIZE)
+ * Every trajectory still performs exactly its own reference sequence of operations. */
+int noc_ipm_rollout(const noc_family* fam, const noc_ipm_ws* ws, void* stream);
+int noc_ipm_step_main(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal,
+                      void* stream);
+int noc_ipm_promote(const noc_ipm_ws* ws, void* stream);
 
 #ifdef __cplusplus
 }

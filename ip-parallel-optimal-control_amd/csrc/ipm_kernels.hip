@@ -135,24 +135,53 @@ struct Fam {
 };
 
 // ------------------------------------------------------------------------------------------------
+NOC_DEV double readlane_d(double v, int lane) {  // wave-uniform broadcast of one lane's double
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Rollout x_{k+1} = f(x_k, u_k) (noc/utils.py:57-63), one wave64 per trajectory.  The recurrence
+// is inherently sequential; every lane evaluates it redundantly (free in SIMD) with u_k broadcast
+// from registers (v_readlane), so the dependent chain never waits on memory: controls are read and
+// states written 64 stages at a time, coalesced.
 template <int KIND, int NX, int NU>
 __global__ __launch_bounds__(256) void rollout_kernel(noc_family prm, noc_ipm_ws w) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= w.Bt || w.phase[b] != NOC_PHASE_ROLLOUT) return;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= w.Bt || w.phase[b] != NOC_PHASE_ROLLOUT) return;  // uniform per wave
   Fam<KIND, NX, NU> f(prm);
   const int N = w.N;
   double x[NX];
   NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = w.x0[(size_t)b * NX + i];
   double* X = w.x + (size_t)b * (N + 1) * NX;
   const double* U = w.u + (size_t)b * N * NU;
-  NOC_UNROLL for (int i = 0; i < NX; ++i) X[i] = x[i];
-  for (int k = 0; k < N; ++k) {
-    double u[NU], xn[NX];
-    NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = U[(size_t)k * NU + j];
-    f.step(x, u, xn);
-    NOC_UNROLL for (int i = 0; i < NX; ++i) { x[i] = xn[i]; X[(size_t)(k + 1) * NX + i] = xn[i]; }
+  if (lane < NX) X[lane] = x[lane];
+  for (int base = 0; base < N; base += 64) {
+    const int k = base + lane;
+    double uk[NU];
+    NOC_UNROLL for (int j = 0; j < NU; ++j) uk[j] = (k < N) ? U[(size_t)k * NU + j] : 0.0;
+    double mine[NX];
+    NOC_UNROLL for (int i = 0; i < NX; ++i) mine[i] = 0.0;
+    const int cnt = (N - base < 64) ? (N - base) : 64;
+    for (int t = 0; t < cnt; ++t) {
+      double ut[NU], xn[NX];
+      NOC_UNROLL for (int j = 0; j < NU; ++j) ut[j] = readlane_d(uk[j], t);
+      f.step(x, ut, xn);
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        x[i] = xn[i];
+        mine[i] = (lane == t) ? xn[i] : mine[i];
+      }
+    }
+    if (k < N) NOC_UNROLL for (int i = 0; i < NX; ++i) X[(size_t)(k + 1) * NX + i] = mine[i];
   }
-  w.phase[b] = NOC_PHASE_LINEARIZE;
+  if (lane == 0) w.phase[b] = NOC_PHASE_ROLLED;
+}
+
+__global__ __launch_bounds__(256) void promote_kernel(noc_ipm_ws w) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < w.Bt && w.phase[b] == NOC_PHASE_ROLLED) w.phase[b] = NOC_PHASE_LINEARIZE;
 }
 
 // thread per (trajectory, chunk slot, lane) in tiled order: the A/B stores are coalesced
@@ -173,71 +202,148 @@ __global__ __launch_bounds__(256) void linearize_kernel(noc_family prm, noc_ipm_
   double x[NX], u[NU];
   gload<NX>(w.x + ((size_t)b * (N + 1) + k) * NX, x);
   NOC_UNROLL for (int i = 0; i < NU; ++i) u[i] = w.u[tn * NU + i];
-  double fx[NX * NX], fu[NX * NU], cx[NX], cu[NU];
+  double fx[NX * NX], fu[NX * NU], cx[NX], cu[NU];  // all stored tiled
   f.jac(x, u, fx, fu);
   f.stage_grad(x, u, bp, cx, cu);
   tstore_rt<NX * NX>(w.A, L, ch.cmax, b, j, l, fx);
   tstore_rt<NX * NU>(w.B, L, ch.cmax, b, j, l, fu);
-  gstore<NX>(w.cx + tn * NX, cx);
-  NOC_UNROLL for (int i = 0; i < NU; ++i) w.cu[tn * NU + i] = cu[i];
-  w.lc[tn] = f.stage_cost(x, u, bp);
+  tstore_rt<NX>(w.cx, L, ch.cmax, b, j, l, cx);
+  tstore_rt<NU>(w.cu, L, ch.cmax, b, j, l, cu);
+  const double lc = f.stage_cost(x, u, bp);
+  tstore_rt<1>(w.lc, L, ch.cmax, b, j, l, &lc);
 }
 
-// one thread per trajectory: sequential costate recursion (C:43-54) + per-trajectory scalars
-template <int KIND, int NX, int NU>
-__global__ __launch_bounds__(256) void costate_kernel(noc_family prm, noc_ipm_ws w, int mode) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= w.Bt || w.phase[b] != NOC_PHASE_LINEARIZE) return;
+// Costates as a reverse affine scan over the horizon (the par_costates pattern, C:34-40),
+// one L-lane segment per trajectory with the KKT scan's chunk geometry (tiled A, B, cx, cu, lc):
+//   lambda_k = cx_k + A_k' lambda_{k+1},  lambda_N = grad final_cost (C:44-52)
+// plus, per trajectory: ru_k = cu_k + B_k' lambda_{k+1} (P:34, tiled), total cost (P:142),
+// max|ru| (P:158), ||cu||_F (P:116), the regularisation fed to the KKT solve and the terminal
+// Hessian hessian(final_cost) (S:66).
+template <int KIND, int NX, int NU, int L>
+__global__ __launch_bounds__(64) void costate_scan_kernel(noc_family prm, noc_ipm_ws w, int mode) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = tid / L, l = tid % L;
+  if (b >= w.Bt || w.phase[b] != NOC_PHASE_LINEARIZE) return;  // uniform per segment
   Fam<KIND, NX, NU> f(prm);
   const int N = w.N;
-  const size_t bN = (size_t)b * N;
-  const Chunks ch(N, w.lanes);
+  const Chunks ch(N, L);
+  const int start = ch.start(l), len = ch.len(l);
+  const bool last = (l == L - 1);
   const double* xN = w.x + ((size_t)b * (N + 1) + N) * NX;
-  double xf[NX], lam[NX];
-  NOC_UNROLL for (int i = 0; i < NX; ++i) xf[i] = xN[i];
-  // lambda_N = grad final_cost (C:44); terminal Hessian = hessian(final_cost) (S:66)
-  NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = prm.wf[i] * f.err(xf, i);
-  double* L = w.lam + (size_t)b * (N + 1) * NX;
-  NOC_UNROLL for (int i = 0; i < NX; ++i) L[(size_t)N * NX + i] = lam[i];
-  double P[NX * NX];
-  NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) P[i * NX + j] = (i == j) ? prm.wf[i] : 0.0;
-  gstore<NX * NX>(w.P + (size_t)b * NX * NX, P);
-  double cost = f.final_cost(xf);
-  double hu = 0.0, g2 = 0.0;
-  for (int k = N - 1; k >= 0; --k) {
-    const size_t t = bN + k;
-    double A[NX * NX], Bm[NX * NU], cx[NX], rr[NU];
-    int l, j;
-    ch.owner(k, l, j);
-    tload_rt<NX * NX>(w.A, w.lanes, ch.cmax, b, j, l, A);
-    tload_rt<NX * NU>(w.B, w.lanes, ch.cmax, b, j, l, Bm);
-    gload<NX>(w.cx + t * NX, cx);
-    // ru_k = cu_k + fu_k' lambda_{k+1}  (P:34)
-    NOC_UNROLL for (int jj = 0; jj < NU; ++jj) {
-      const double cu = w.cu[t * NU + jj];
-      double r = cu;
+  double lamN[NX];
+  NOC_UNROLL for (int i = 0; i < NX; ++i) lamN[i] = prm.wf[i] * f.err(xN, i);
+  // phase 1: chunk map lambda_start = G lambda_end + g
+  Mat<NX, NX> G;
+  Vec<NX> g;
+  set_identity(G);
+  set_zero(g);
+  for (int k = start + len - 1; k >= start; --k) {
+    double A[NX * NX], cx[NX];
+    tload_rt<NX * NX>(w.A, L, ch.cmax, b, k - start, l, A);
+    tload_rt<NX>(w.cx, L, ch.cmax, b, k - start, l, cx);
+    Mat<NX, NX> Gn;
+    Vec<NX> gn;
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      double t = cx[i];
+      NOC_UNROLL for (int m = 0; m < NX; ++m) t += A[m * NX + i] * g[m];
+      gn[i] = t;
+      NOC_UNROLL for (int j = 0; j < NX; ++j) {
+        double u = 0.0;
+        NOC_UNROLL for (int m = 0; m < NX; ++m) u += A[m * NX + i] * G(m, j);
+        Gn(i, j) = u;
+      }
+    }
+    G = Gn;
+    g = gn;
+  }
+  if (last) {  // the last chunk ends at the terminal costate: its map becomes constant
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      double t = g[i];
+      NOC_UNROLL for (int m = 0; m < NX; ++m) t += G(i, m) * lamN[m];
+      g[i] = t;
+    }
+    set_zero(G);
+  }
+  // phase 2: reverse Hillis-Steele; lanes without a partner get their own (already constant) map
+#pragma unroll 1
+  for (int d = 1; d < L; d <<= 1) {
+    Mat<NX, NX> G2;
+    Vec<NX> g2;
+    shfl_down_arr<NX * NX>(G.v, G2.v, d, L);
+    shfl_down_arr<NX>(g.v, g2.v, d, L);
+    Mat<NX, NX> Gn;
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      double t = g[i];
+      NOC_UNROLL for (int m = 0; m < NX; ++m) t += G(i, m) * g2[m];
+      g[i] = t;
+      NOC_UNROLL for (int j = 0; j < NX; ++j) {
+        double u = 0.0;
+        NOC_UNROLL for (int m = 0; m < NX; ++m) u += G(i, m) * G2(m, j);
+        Gn(i, j) = u;
+      }
+    }
+    G = Gn;
+  }
+  // phase 3: sweep the chunk from its true end costate
+  double lam[NX];
+  shfl_down_arr<NX>(g.v, lam, 1, L);
+  if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = lamN[i];
+  double* LAM = w.lam + (size_t)b * (N + 1) * NX;
+  if (last) gstore<NX>(LAM + (size_t)N * NX, lamN);
+  double cost = 0.0, hu = 0.0, g2s = 0.0;
+  for (int k = start + len - 1; k >= start; --k) {
+    double A[NX * NX], Bm[NX * NU], cx[NX], cu[NU], lc, rr[NU];
+    tload_rt<NX * NX>(w.A, L, ch.cmax, b, k - start, l, A);
+    tload_rt<NX * NU>(w.B, L, ch.cmax, b, k - start, l, Bm);
+    tload_rt<NX>(w.cx, L, ch.cmax, b, k - start, l, cx);
+    tload_rt<NU>(w.cu, L, ch.cmax, b, k - start, l, cu);
+    tload_rt<1>(w.lc, L, ch.cmax, b, k - start, l, &lc);
+    NOC_UNROLL for (int jj = 0; jj < NU; ++jj) {  // ru_k = cu_k + fu_k' lambda_{k+1}  (P:34)
+      double r = cu[jj];
       NOC_UNROLL for (int i = 0; i < NX; ++i) r += Bm[i * NU + jj] * lam[i];
       rr[jj] = r;
       hu = fmax(hu, fabs(r));
-      g2 += cu * cu;
+      g2s += cu[jj] * cu[jj];
     }
-    tstore_rt<NU>(w.r, w.lanes, ch.cmax, b, j, l, rr);
+    tstore_rt<NU>(w.r, L, ch.cmax, b, k - start, l, rr);
     double ln[NX];
     NOC_UNROLL for (int i = 0; i < NX; ++i) {
-      double s = cx[i];
-      NOC_UNROLL for (int m = 0; m < NX; ++m) s += A[m * NX + i] * lam[m];
-      ln[i] = s;
+      double t = cx[i];
+      NOC_UNROLL for (int m = 0; m < NX; ++m) t += A[m * NX + i] * lam[m];
+      ln[i] = t;
     }
-    NOC_UNROLL for (int i = 0; i < NX; ++i) { lam[i] = ln[i]; L[(size_t)k * NX + i] = ln[i]; }
-    cost += w.lc[t];
+    NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = ln[i];
+    gstore<NX>(LAM + (size_t)k * NX, lam);
+    cost += lc;
   }
-  w.cost[b] = cost;                 // total_cost(x, u, bp) (P:142)
-  w.hu[b] = hu;                     // max |Hu| (P:158)
-  const double gn = sqrt(g2);       // ||cu||_F (P:116)
+  NOC_UNROLL for (int off = L / 2; off > 0; off >>= 1) {
+    cost += __shfl_xor(cost, off, L);
+    g2s += __shfl_xor(g2s, off, L);
+    hu = fmax(hu, __shfl_xor(hu, off, L));
+  }
+  if (l != 0) return;
+  double P[NX * NX];
+  NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) P[i * NX + j] = (i == j) ? prm.wf[i] : 0.0;
+  gstore<NX * NX>(w.P + (size_t)b * NX * NX, P);
+  w.cost[b] = cost + f.final_cost(xN);   // total_cost(x, u, bp) (P:142)
+  w.hu[b] = hu;                          // max |Hu| (P:158)
+  const double gn = sqrt(g2s);           // ||cu||_F (P:116)
   w.gnorm[b] = gn;
   // regularisation fed to the KKT solve: par R += rp*||cu||*I (P:116-118); seq Quu += mu*I (S:51)
   w.reg[b] = (mode == NOC_MODE_PAR) ? w.rp[b] * gn : w.rp[b];
   w.inner[b] = 0;
+}
+
+template <int KIND, int NX, int NU>
+static void launch_costate(const noc_family& p, const noc_ipm_ws& w, int mode, hipStream_t s) {
+  const int L = w.lanes;
+  const unsigned grid = (unsigned)(((long long)w.Bt * L + 63) / 64);
+  switch (L) {
+    case 64: hipLaunchKernelGGL((costate_scan_kernel<KIND, NX, NU, 64>), dim3(grid), dim3(64), 0, s, p, w, mode); break;
+    case 32: hipLaunchKernelGGL((costate_scan_kernel<KIND, NX, NU, 32>), dim3(grid), dim3(64), 0, s, p, w, mode); break;
+    case 16: hipLaunchKernelGGL((costate_scan_kernel<KIND, NX, NU, 16>), dim3(grid), dim3(64), 0, s, p, w, mode); break;
+    default: hipLaunchKernelGGL((costate_scan_kernel<KIND, NX, NU, 8>), dim3(grid), dim3(64), 0, s, p, w, mode); break;
+  }
 }
 
 template <int KIND, int NX, int NU>
@@ -281,7 +387,7 @@ __global__ __launch_bounds__(256) void mark_solve_kernel(noc_ipm_ws w) {
   if (b >= w.Bt) return;
   const int ph = w.phase[b];
   if (ph == NOC_PHASE_LINEARIZE) w.phase[b] = NOC_PHASE_SOLVE;
-  w.kkt_active[b] = (ph == NOC_PHASE_DONE) ? 0 : 1;
+  w.kkt_active[b] = (ph == NOC_PHASE_LINEARIZE || ph == NOC_PHASE_SOLVE) ? 1 : 0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -394,17 +500,32 @@ __global__ __launch_bounds__(256) void init_kernel(noc_ipm_ws w, double bp0) {
 
 // ------------------------------------------------------------------------------------------------
 template <int KIND, int NX, int NU>
-static hipError_t prepare_t(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
-                            hipStream_t s) {
+static hipError_t rollout_t(const noc_family& p, const noc_ipm_ws& w, hipStream_t s) {
+  hipLaunchKernelGGL((rollout_kernel<KIND, NX, NU>), dim3((w.Bt + 3) / 4), dim3(256), 0, s, p, w);
+  return hipGetLastError();
+}
+
+// linearise + costates + LQ blocks for phase-LINEARIZE trajectories, then LINEARIZE -> SOLVE
+template <int KIND, int NX, int NU>
+static hipError_t prepare_main_t(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                                 hipStream_t s) {
   const int bt_grid = (w.Bt + 255) / 256;
   const long long cmax = (w.N + w.lanes - 1) / w.lanes;
   const unsigned st_grid = (unsigned)(((long long)w.Bt * cmax * w.lanes + 255) / 256);
-  hipLaunchKernelGGL((rollout_kernel<KIND, NX, NU>), dim3(bt_grid), dim3(256), 0, s, p, w);
   hipLaunchKernelGGL((linearize_kernel<KIND, NX, NU>), dim3(st_grid), dim3(256), 0, s, p, w);
-  hipLaunchKernelGGL((costate_kernel<KIND, NX, NU>), dim3(bt_grid), dim3(256), 0, s, p, w, mode);
+  launch_costate<KIND, NX, NU>(p, w, mode, s);
   hipLaunchKernelGGL((assemble_kernel<KIND, NX, NU>), dim3(st_grid), dim3(256), 0, s, p, w, terminal);
   hipLaunchKernelGGL(mark_solve_kernel, dim3(bt_grid), dim3(256), 0, s, w);
   return hipGetLastError();
+}
+
+template <int KIND, int NX, int NU>
+static hipError_t prepare_t(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                            hipStream_t s) {
+  hipError_t e = rollout_t<KIND, NX, NU>(p, w, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(promote_kernel, dim3((w.Bt + 255) / 256), dim3(256), 0, s, w);
+  return prepare_main_t<KIND, NX, NU>(p, w, mode, terminal, s);
 }
 
 template <int KIND, int NX, int NU>
@@ -430,6 +551,46 @@ hipError_t ipm_prepare(const noc_family& p, const noc_ipm_ws& w, int mode, int t
     default: break;
   }
   return hipErrorInvalidValue;
+}
+
+hipError_t ipm_rollout(const noc_family& p, const noc_ipm_ws& w, hipStream_t s) {
+  switch (p.kind) {
+    case NOC_FAMILY_PENDULUM:
+      if (p.nx == 2 && p.nu == 1) return rollout_t<NOC_FAMILY_PENDULUM, 2, 1>(p, w, s);
+      break;
+    case NOC_FAMILY_CARTPOLE:
+      if (p.nx == 4 && p.nu == 1) return rollout_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, w, s);
+      break;
+    case NOC_FAMILY_LINEAR:
+      if (p.nx == 2 && p.nu == 1) return rollout_t<NOC_FAMILY_LINEAR, 2, 1>(p, w, s);
+      if (p.nx == 8 && p.nu == 4) return rollout_t<NOC_FAMILY_LINEAR, 8, 4>(p, w, s);
+      break;
+    default: break;
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t ipm_prepare_main(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                            hipStream_t s) {
+  switch (p.kind) {
+    case NOC_FAMILY_PENDULUM:
+      if (p.nx == 2 && p.nu == 1) return prepare_main_t<NOC_FAMILY_PENDULUM, 2, 1>(p, w, mode, terminal, s);
+      break;
+    case NOC_FAMILY_CARTPOLE:
+      if (p.nx == 4 && p.nu == 1) return prepare_main_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, w, mode, terminal, s);
+      break;
+    case NOC_FAMILY_LINEAR:
+      if (p.nx == 2 && p.nu == 1) return prepare_main_t<NOC_FAMILY_LINEAR, 2, 1>(p, w, mode, terminal, s);
+      if (p.nx == 8 && p.nu == 4) return prepare_main_t<NOC_FAMILY_LINEAR, 8, 4>(p, w, mode, terminal, s);
+      break;
+    default: break;
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t ipm_promote(const noc_ipm_ws& w, hipStream_t s) {
+  hipLaunchKernelGGL(promote_kernel, dim3((w.Bt + 255) / 256), dim3(256), 0, s, w);
+  return hipGetLastError();
 }
 
 hipError_t ipm_trial(const noc_family& p, const noc_ipm_ws& w, int mode, hipStream_t s) {

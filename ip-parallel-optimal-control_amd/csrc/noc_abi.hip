@@ -224,11 +224,48 @@ int noc_ipm_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* s
   return hip_status(noc::ipm_trial(*fam, *ws, mode, static_cast<hipStream_t>(stream)), "ipm_trial");
 }
 
+static int kkt_and_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* stream);
+
 int noc_ipm_step(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, int lanes,
                  void* stream) {
+  (void)lanes;
   int rc = noc_ipm_prepare(fam, ws, mode, terminal, stream);
   if (rc) return rc;
-  (void)lanes;  // the KKT scan must use the workspace's tiled lane count
+  return kkt_and_trial(fam, ws, mode, stream);
+}
+
+int noc_ipm_rollout(const noc_family* fam, const noc_ipm_ws* ws, void* stream) {
+  if (!fam) return fail(-2, "family is NULL");
+  int rc = check_ipm(fam, ws);
+  if (rc) return rc;
+  if (ws->Bt == 0) return 0;
+  return hip_status(noc::ipm_rollout(*fam, *ws, static_cast<hipStream_t>(stream)), "ipm_rollout");
+}
+
+int noc_ipm_promote(const noc_ipm_ws* ws, void* stream) {
+  int rc = check_ipm(nullptr, ws);
+  if (rc) return rc;
+  if (ws->Bt == 0) return 0;
+  return hip_status(noc::ipm_promote(*ws, static_cast<hipStream_t>(stream)), "ipm_promote");
+}
+
+int noc_ipm_step_main(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal,
+                      void* stream) {
+  if (!fam) return fail(-2, "family is NULL");
+  int rc = check_ipm(fam, ws);
+  if (rc) return rc;
+  if (mode != NOC_MODE_PAR && mode != NOC_MODE_SEQ) return fail(-1, "bad mode");
+  if (terminal != NOC_TERMINAL_FINAL_COST && terminal != NOC_TERMINAL_STAGE0)
+    return fail(-1, "bad terminal option");
+  if (ws->Bt == 0) return 0;
+  rc = hip_status(noc::ipm_prepare_main(*fam, *ws, mode, terminal, static_cast<hipStream_t>(stream)),
+                  "ipm_prepare_main");
+  if (rc) return rc;
+  return kkt_and_trial(fam, ws, mode, stream);
+}
+
+static int kkt_and_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* stream) {
+  int rc;
   rc = noc_kkt_solve_tiled(fam->nx, fam->nu, ws->N, ws->Bt, ws->lanes, ws->A, ws->B, ws->Q, ws->R, ws->M,
                      ws->r, nullptr, nullptr, ws->P, nullptr, nullptr, ws->reg, ws->kkt_active,
                      ws->dx, ws->du, ws->pred, ws->feasible, ws->K, ws->d, nullptr, nullptr,

@@ -30,6 +30,10 @@ int kkt_default_lanes(int nx, int nu, int N);
 hipError_t ipm_prepare(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                        hipStream_t s);
 hipError_t ipm_trial(const noc_family& p, const noc_ipm_ws& w, int mode, hipStream_t s);
+hipError_t ipm_rollout(const noc_family& p, const noc_ipm_ws& w, hipStream_t s);
+hipError_t ipm_prepare_main(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                            hipStream_t s);
+hipError_t ipm_promote(const noc_ipm_ws& w, hipStream_t s);
 hipError_t ipm_init(const noc_ipm_ws& w, double bp0, hipStream_t s);
 hipError_t relayout(int direction, int E, int sym_n, int N, int Bt, int L, const double* src,
                     double* dst, hipStream_t s);

@@ -33,7 +33,7 @@ SIGNATURES = {
 
 # --- structs of include/noc_hip.h --------------------------------------------------------------
 FAMILY_PENDULUM, FAMILY_CARTPOLE, FAMILY_LINEAR = 1, 2, 3
-PHASE_ROLLOUT, PHASE_LINEARIZE, PHASE_SOLVE, PHASE_DONE = 0, 1, 2, 3
+PHASE_ROLLOUT, PHASE_LINEARIZE, PHASE_SOLVE, PHASE_DONE, PHASE_ROLLED = 0, 1, 2, 3, 4
 MODE_PAR, MODE_SEQ = 0, 1
 TERMINAL_FINAL_COST, TERMINAL_STAGE0 = 0, 1
 
@@ -66,6 +66,9 @@ SIGNATURES.update({
     "noc_ipm_prepare": (_i, [_fp, _wp, _i, _i, _dp]),
     "noc_ipm_trial": (_i, [_fp, _wp, _i, _dp]),
     "noc_ipm_step": (_i, [_fp, _wp, _i, _i, _i, _dp]),
+    "noc_ipm_rollout": (_i, [_fp, _wp, _dp]),
+    "noc_ipm_step_main": (_i, [_fp, _wp, _i, _i, _dp]),
+    "noc_ipm_promote": (_i, [_wp, _dp]),
 })
 
 _lib: Optional[ctypes.CDLL] = None

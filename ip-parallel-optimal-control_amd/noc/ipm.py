@@ -19,7 +19,8 @@ from . import _lib
 
 
 class BatchedIPM:
-    def __init__(self, family, N: int, batch: int, device="cuda", lanes: int = 0):
+    def __init__(self, family, N: int, batch: int, device="cuda", lanes: int = 0,
+                 overlap: Optional[bool] = None):
         if not torch.cuda.is_available():
             raise _lib.NocError("no HIP device visible: the MI355X path has no CPU fallback")
         self.family = family
@@ -39,8 +40,8 @@ class BatchedIPM:
         # LQ blocks and gains in the KKT scan's tiled layout (Q, R packed symmetric)
         shapes = dict(x=(Bt, N + 1, nx), u=(Bt, N, nu), x0=(Bt, nx), A=tiled(nx * nx),
                       B=tiled(nx * nu), Q=tiled(nx * (nx + 1) // 2), R=tiled(nu * (nu + 1) // 2),
-                      M=tiled(nx * nu), r=tiled(nu), P=(Bt, nx, nx), cx=(Bt, N, nx),
-                      cu=(Bt, N, nu), lc=(Bt, N), lam=(Bt, N + 1, nx), dx=(Bt, N + 1, nx),
+                      M=tiled(nx * nu), r=tiled(nu), P=(Bt, nx, nx), cx=tiled(nx),
+                      cu=tiled(nu), lc=tiled(1), lam=(Bt, N + 1, nx), dx=(Bt, N + 1, nx),
                       du=(Bt, N, nu), pred=(Bt,), K=tiled(nu * nx), d=tiled(nu))
         self.t = {k: torch.zeros(s, **f64) for k, s in shapes.items()}
         for k in _lib.WS_INT_FIELDS:
@@ -53,6 +54,14 @@ class BatchedIPM:
             setattr(ws, k, self.t[k].data_ptr())
         self.ws = ws
         self._lib = lib
+        # overlapping rollouts on a second stream pays once a Newton step costs more than the
+        # extra launch + event overhead (measured: c3 B*N = 819k faster, c2 B*N = 102k slower)
+        self.overlap = (Bt * N >= 256 * 1024) if overlap is None else bool(overlap)
+        if self.overlap:
+            self.roll_stream = torch.cuda.Stream(device=self.device)
+            self.ev_roll = torch.cuda.Event()
+            self.ev_main = torch.cuda.Event()
+            self.ev_main.record(torch.cuda.current_stream(self.device))
 
     # -------------------------------------------------------------------------------------------
     def load(self, controls, initial_state):
@@ -67,14 +76,34 @@ class BatchedIPM:
     def init(self, bp0: float = 0.1):
         _lib.check(self._lib.noc_ipm_init(ctypes.byref(self.ws), float(bp0), self._stream()),
                    "noc_ipm_init")
+        if self.overlap:  # the roll stream must see load() + init() before its first rollout
+            self.ev_main.record(torch.cuda.current_stream(self.device))
 
     def prepare(self, mode: int, terminal: int):
         _lib.check(self._lib.noc_ipm_prepare(ctypes.byref(self.fam_c), ctypes.byref(self.ws), mode,
                                              terminal, self._stream()), "noc_ipm_prepare")
 
     def step(self, mode: int, terminal: int):
-        _lib.check(self._lib.noc_ipm_step(ctypes.byref(self.fam_c), ctypes.byref(self.ws), mode,
-                                          terminal, self.lanes, self._stream()), "noc_ipm_step")
+        """One device iteration.  With overlap (default) the rollouts of trajectories that start
+        a barrier stage run on a second stream beside the other trajectories' Newton step."""
+        if not self.overlap:
+            _lib.check(self._lib.noc_ipm_step(ctypes.byref(self.fam_c), ctypes.byref(self.ws),
+                                              mode, terminal, self.lanes, self._stream()),
+                       "noc_ipm_step")
+            return
+        main = torch.cuda.current_stream(self.device)
+        roll = self.roll_stream
+        roll.wait_event(self.ev_main)
+        _lib.check(self._lib.noc_ipm_rollout(ctypes.byref(self.fam_c), ctypes.byref(self.ws),
+                                             roll.cuda_stream), "noc_ipm_rollout")
+        self.ev_roll.record(roll)
+        _lib.check(self._lib.noc_ipm_step_main(ctypes.byref(self.fam_c), ctypes.byref(self.ws),
+                                               mode, terminal, main.cuda_stream),
+                   "noc_ipm_step_main")
+        main.wait_event(self.ev_roll)
+        _lib.check(self._lib.noc_ipm_promote(ctypes.byref(self.ws), main.cuda_stream),
+                   "noc_ipm_promote")
+        self.ev_main.record(main)
 
     def active_count(self) -> int:
         return int((self.t["phase"] != _lib.PHASE_DONE).sum().item())

@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""End-to-end batched interior-point solve timing (device loop), per-kernel breakdown via
+rocprofv3 when run under it.  Prints one JSON line."""
+import json, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ip-parallel-optimal-control_amd"))
+import numpy as np
+import torch
+from noc import problems, _lib
+from noc.ipm import BatchedIPM
+
+name = sys.argv[1] if len(sys.argv) > 1 else "cartpole"
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+B = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
+ocp = problems.make_problem(name, N)
+x0, u0 = problems.initial_conditions(name, N, B, seed=11)
+eng = BatchedIPM(ocp.family, N, B)
+eng.load(u0, x0)
+eng.solve(max_steps=16)   # warm-up (kernels loaded, caches)
+torch.cuda.synchronize()
+eng.load(u0, x0)
+t0 = time.perf_counter()
+steps = eng.solve()
+torch.cuda.synchronize()
+dt = time.perf_counter() - t0
+U, its, solves = (t.cpu().numpy() for t in eng.result())
+print(json.dumps({"problem": name, "N": N, "B": B, "lanes": eng.lanes, "device_steps": steps,
+                  "wall_s": dt, "ms_per_device_step": 1e3 * dt / steps,
+                  "total_kkt_solves": int(solves.sum()), "kkt_solves_per_s": float(solves.sum() / dt),
+                  "mean_outer_iters": float(its.mean()), "max_kkt_solves": int(solves.max()),
+                  "min_kkt_solves": int(solves.min())}))
