@@ -98,13 +98,13 @@ def main():
     tb = blocks["tiled"]
     nx, nu, lanes = tb.nx, tb.nu, tb.lanes
     if args.layout == "tiled":
-        out = lqt.kkt_solve_tiled(tb, reg=blocks["reg"])
+        out = lqt.kkt_solve_tiled(tb, reg=blocks["reg"], want_gains=False)
 
         def step():
             lqt.kkt_solve_tiled(tb, reg=blocks["reg"], out=out)
     else:
         nat = [blocks[k] for k in ("A", "B", "Q", "R", "M", "r", "P")]
-        out = lqt.kkt_solve(*nat, reg=blocks["reg"], lanes=lanes)
+        out = lqt.kkt_solve(*nat, reg=blocks["reg"], lanes=lanes, want_gains=False)
 
         def step():
             lqt.kkt_solve(*nat, reg=blocks["reg"], lanes=lanes, out=out)

@@ -16,7 +16,9 @@
  *   reg [B] (NULL = 0)                              active [B] int32 (NULL = all; 0 = skip)
  * Outputs:
  *   dx [B][N+1][nx]  du [B][N][nu]  pred [B]  feasible [B] int32
- *   K [B][N][nu][nx] d [B][N][nu]   (du_k = K_k dx_k + d_k)   -- always written (workspace)
+ *   K [B][N][nu][nx] d [B][N][nu]   (du_k = K_k dx_k + d_k); NULL = not written, allowed in
+ *                                   the fused solves when noc_kkt_gains_on_chip() is 1 (the
+ *                                   gains then never leave the CU: par_Newton discards them)
  *   S [B][N+1][nx][nx]  v [B][N+1][nx]  (V_k(x) = 1/2 x'S_k x + v_k'x; NULL = not written)
  *   pred = sum_k d_k'Qu_k + 1/2 d_k'Quu_k d_k,  feasible = all_k Quu_k > 0
  *
@@ -37,6 +39,9 @@ int noc_abi_version(void);
 const char* noc_last_error(void);
 int noc_kkt_supported(int nx, int nu);
 int noc_kkt_default_lanes(int nx, int nu, int N);
+/* 1 if the fused solve (noc_kkt_solve / _tiled) with these sizes keeps the gains K, d in LDS
+ * between its backward and forward phases, so K and d may be passed as NULL. */
+int noc_kkt_gains_on_chip(int nx, int nu, int N, int lanes);
 /* Timing-only phase ablation of the KKT scan (bit0: skip the cross-lane scan, bit1: skip the
  * forward pass, bit2: stop after the in-chunk elements).  Results are WRONG while set; used by
  * tools/kkt_ablate.py to attribute kernel time to phases.  0 (default) in every product call. */

@@ -331,8 +331,20 @@ NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
   }
 }
 
+// On-chip slot region of one trajectory (one per L-lane segment of the 64-thread block): N slots
+// of KD = NU*(NX+1) doubles (K_s, d_s after phase 3, then x_s, u_s in phase 4) + x_N.
+template <int NX, int NU>
+NOC_DEV constexpr int kd_width() { return NU * (NX + 1); }
+template <int NX, int NU, int L>
+NOC_DEV double* lds_slots(int N) {
+  extern __shared__ __attribute__((aligned(16))) double noc_smem[];
+  const int per_traj = (N * kd_width<NX, NU>() + NX + 1) & ~1;
+  return noc_smem + (size_t)(threadIdx.x / L) * per_traj;
+}
+
 template <int NX, int NU, int L, bool AFF, bool TILED>
 __global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
+  constexpr int KD = kd_width<NX, NU>();
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int traj = tid / L;
   const int l = tid % L;
@@ -396,6 +408,7 @@ __global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KK
     set_zero(phi);
     double pred = 0.0;
     int feas = 1;
+    double* skd = lds_slots<NX, NU, L>(N);  // K, d stay on chip for phase 4 when staged
     for (int s = start + len - 1; s >= start; --s) {
       StageData<NX, NU> st;
       load_stage<NX, NU, L, AFF, TILED>(a, traj, tN + s, s - start, l, cmax, reg, st);
@@ -449,7 +462,10 @@ __global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KK
         NOC_UNROLL for (int j = 0; j < NX; ++j) Kk[i * NX + j] = -Y[i][j];
         Kk[NU * NX + i] = -Y[i][NX];
       }
-      store_Kd<NX, NU, L, TILED>(a, traj, tN + s, s - start, l, cmax, Kk);
+      if (a.lds_out) {
+        NOC_UNROLL for (int i = 0; i < NU * (NX + 1); ++i) skd[s * KD + i] = Kk[i];
+      }
+      if (a.K) store_Kd<NX, NU, L, TILED>(a, traj, tN + s, s - start, l, cmax, Kk);
       // dV = k'Qu + 1/2 k'Quu k   (noc/seq_interior_point_newton.py:63)
       NOC_UNROLL for (int i = 0; i < NU; ++i) {
         const double ki = Kk[NU * NX + i];
@@ -585,32 +601,32 @@ __global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KK
   Vec<NX> x;
   shfl_up_arr<NX>(phi.v, x.v, 1, L);
   if (l == 0) x = x0;
-  // dx/du rows go through LDS (one region per trajectory segment) and leave as whole contiguous
-  // rows: per-lane direct stores would touch one cache line per lane per store instruction.
-  extern __shared__ __attribute__((aligned(16))) double noc_smem[];
-  const int rows_dx = (N + 1) * NX, rows_du = N * NU;
-  const int per_traj = (rows_dx + rows_du + 1) & ~1;
-  double* sdx = noc_smem + (size_t)(threadIdx.x / L) * per_traj;
-  double* sdu = sdx + rows_dx;
+  // dx/du rows go through LDS (slot s of the trajectory's region holds K_s, d_s from phase 3 and
+  // is overwritten by x_s, u_s here) and leave as whole contiguous rows: per-lane direct stores
+  // would touch one cache line per lane per store instruction.
+  double* slot = lds_slots<NX, NU, L>(N);
   const bool via_lds = a.lds_out != 0;
+  const bool kd_lds = via_lds && a.mode == MODE_FULL;
   Mat<NX, NX> nA;
   Mat<NX, NU> nB;
   double nK[NU * (NX + 1)];
   Vec<NX> nc;
-  if (len > 0) {
-    load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + start, 0, l, cmax, nA, nB, nc);
-    load_Kd<NX, NU, L, TILED>(a, traj, tN + start, 0, l, cmax, nK);
-  }
+  auto fetch = [&](int s) {
+    load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + s, s - start, l, cmax, nA, nB, nc);
+    if (kd_lds) {
+      NOC_UNROLL for (int i = 0; i < NU * (NX + 1); ++i) nK[i] = slot[s * KD + i];
+    } else {
+      load_Kd<NX, NU, L, TILED>(a, traj, tN + s, s - start, l, cmax, nK);
+    }
+  };
+  if (len > 0) fetch(start);
   for (int s = start; s < start + len; ++s) {
     const Mat<NX, NX> A = nA;
     const Mat<NX, NU> Bm = nB;
     const Vec<NX> cc = nc;
     double Kk[NU * (NX + 1)];
     NOC_UNROLL for (int i = 0; i < NU * (NX + 1); ++i) Kk[i] = nK[i];
-    if (s + 1 < start + len) {  // prefetch the next stage
-      load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + s + 1, s + 1 - start, l, cmax, nA, nB, nc);
-      load_Kd<NX, NU, L, TILED>(a, traj, tN + s + 1, s + 1 - start, l, cmax, nK);
-    }
+    if (s + 1 < start + len) fetch(s + 1);  // prefetch the next stage
     Vec<NU> u;
     NOC_UNROLL for (int i = 0; i < NU; ++i) {
       double t = Kk[NU * NX + i];
@@ -618,8 +634,8 @@ __global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KK
       u[i] = t;
     }
     if (via_lds) {
-      NOC_UNROLL for (int i = 0; i < NX; ++i) sdx[s * NX + i] = x[i];
-      NOC_UNROLL for (int i = 0; i < NU; ++i) sdu[s * NU + i] = u[i];
+      NOC_UNROLL for (int i = 0; i < NX; ++i) slot[s * KD + i] = x[i];
+      NOC_UNROLL for (int i = 0; i < NU; ++i) slot[s * KD + NX + i] = u[i];
     } else {
       if (a.dx) gstore<NX>(a.dx + (tN + traj + s) * NX, x.v);
       if (a.du) gstore<NU>(a.du + (tN + s) * NU, u.v);
@@ -637,28 +653,34 @@ __global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KK
     if (last && a.dx) gstore<NX>(a.dx + (tN + traj + N) * NX, x.v);
     return;
   }
-  if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) sdx[N * NX + i] = x[i];
+  if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) slot[N * KD + i] = x[i];
   __syncthreads();  // one wave per block: orders this wave's LDS writes before its reads
   if (a.dx) {
-    const double2* src = reinterpret_cast<const double2*>(sdx);
-    double2* dst = reinterpret_cast<double2*>(a.dx + (tN + traj) * NX);
+    double* dst = a.dx + (tN + traj) * NX;
     if constexpr (NX % 2 == 0) {
-      for (int i = l; i < rows_dx / 2; i += L) dst[i] = src[i];
+      constexpr int H = NX / 2;
+      double2* dst2 = reinterpret_cast<double2*>(dst);
+      for (int i = l; i < (N + 1) * H; i += L) {
+        const int s = i / H, e = 2 * (i - s * H);
+        dst2[i] = make_double2(slot[s * KD + e], slot[s * KD + e + 1]);
+      }
     } else {
-      for (int i = l; i < rows_dx; i += L) a.dx[(tN + traj) * NX + i] = sdx[i];
+      for (int i = l; i < (N + 1) * NX; i += L) {
+        const int s = i / NX;
+        dst[i] = slot[s * KD + (i - s * NX)];
+      }
     }
   }
-  if (a.du)
-    for (int i = l; i < rows_du; i += L) a.du[tN * NU + i] = sdu[i];
+  if (a.du) {
+    double* dst = a.du + tN * NU;
+    for (int i = l; i < N * NU; i += L) {
+      const int s = i / NU;
+      dst[i] = slot[s * KD + NX + (i - s * NU)];
+    }
+  }
 }
 
-// dynamic LDS bytes of one 64-thread block when dx/du are staged (0: stage directly)
-template <int NX, int NU, int L>
-static size_t kkt_lds_bytes(int N) {
-  const size_t per_traj = (size_t)(((N + 1) * NX + N * NU + 1) & ~1);
-  const size_t bytes = (64 / L) * per_traj * sizeof(double);
-  return bytes <= 32768 ? bytes : 0;  // keep >= 4 blocks (waves) per CU resident
-}
+
 
 // ---------------------------------------------------------------------------------------------
 template <int NX, int NU, int L, bool AFF>
@@ -667,8 +689,9 @@ static hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
   const long long threads = (long long)a.B * L;
   const int block = 64;  // one wave per workgroup: waves are independent (no LDS sharing)
   const unsigned grid = (unsigned)((threads + block - 1) / block);
-  const size_t lds = (a.mode == MODE_BWD || (!a.dx && !a.du)) ? 0 : kkt_lds_bytes<NX, NU, L>(a.N);
+  const size_t lds = (a.mode == MODE_BWD || (!a.dx && !a.du)) ? 0 : kkt_lds_bytes_rt(NX, NU, a.N, L);
   a.lds_out = lds > 0 ? 1 : 0;
+  if (!a.lds_out && (!a.K || !a.d)) return hipErrorInvalidValue;  // K/d needed as workspace
   if (a.tiled)
     hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true>), dim3(grid), dim3(block), lds, stream, a);
   else

@@ -71,6 +71,11 @@ void noc_debug_set_ablation(int bits) { g_ablate = bits; }
 const char* noc_last_error(void) { return g_last_error.c_str(); }
 int noc_kkt_supported(int nx, int nu) { return noc::kkt_supported(nx, nu) ? 1 : 0; }
 int noc_kkt_default_lanes(int nx, int nu, int N) { return noc::kkt_default_lanes(nx, nu, N); }
+int noc_kkt_gains_on_chip(int nx, int nu, int N, int lanes) {
+  if (check_dims(nx, nu, N, 1, lanes)) return 0;
+  const int L = lanes ? lanes : noc::kkt_default_lanes(nx, nu, N);
+  return noc::kkt_lds_bytes_rt(nx, nu, N, L) > 0 ? 1 : 0;
+}
 
 static int kkt_common(int mode, int tiled, int nx, int nu, int N, int B, int lanes, const double* A,
                       const double* Bm, const double* Q, const double* R, const double* M,
@@ -93,8 +98,8 @@ static int kkt_common(int mode, int tiled, int nx, int nu, int N, int B, int lan
   if ((rc = check_ptr(c, "c", false))) return rc;
   if ((rc = check_ptr(p, "p", false))) return rc;
   if ((rc = check_ptr(x0, "x0", false))) return rc;
-  if ((rc = check_ptr(K, "K", true))) return rc;
-  if ((rc = check_ptr(d, "d", true))) return rc;
+  if ((rc = check_ptr(K, "K", false))) return rc;
+  if ((rc = check_ptr(d, "d", false))) return rc;
   if ((rc = check_ptr(S, "S", false))) return rc;
   if ((rc = check_ptr(v, "v", false))) return rc;
   if ((rc = check_ptr(dx, "dx", false))) return rc;
@@ -115,6 +120,9 @@ static int kkt_common(int mode, int tiled, int nx, int nu, int N, int B, int lan
   (void)bwd;
   (void)fwd;
   const int L = lanes ? lanes : noc::kkt_default_lanes(nx, nu, N);
+  const bool on_chip = mode == noc::MODE_FULL && (dx || du) && noc::kkt_lds_bytes_rt(nx, nu, N, L) > 0;
+  if ((!K || !d) && !on_chip)
+    return fail(-2, "K and d are required (workspace) unless noc_kkt_gains_on_chip() is 1");
   return hip_status(noc::kkt_dispatch(nx, nu, a, L, static_cast<hipStream_t>(stream)),
                     "kkt_scan launch");
 }
@@ -265,11 +273,13 @@ int noc_ipm_step_main(const noc_family* fam, const noc_ipm_ws* ws, int mode, int
 }
 
 static int kkt_and_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* stream) {
-  int rc;
-  rc = noc_kkt_solve_tiled(fam->nx, fam->nu, ws->N, ws->Bt, ws->lanes, ws->A, ws->B, ws->Q, ws->R, ws->M,
-                     ws->r, nullptr, nullptr, ws->P, nullptr, nullptr, ws->reg, ws->kkt_active,
-                     ws->dx, ws->du, ws->pred, ws->feasible, ws->K, ws->d, nullptr, nullptr,
-                     stream);
+  // the trial step needs dx, du only: gains stay on chip when they fit (ws->K, ws->d otherwise)
+  const bool on_chip = noc_kkt_gains_on_chip(fam->nx, fam->nu, ws->N, ws->lanes) == 1;
+  int rc = noc_kkt_solve_tiled(fam->nx, fam->nu, ws->N, ws->Bt, ws->lanes, ws->A, ws->B, ws->Q,
+                               ws->R, ws->M, ws->r, nullptr, nullptr, ws->P, nullptr, nullptr,
+                               ws->reg, ws->kkt_active, ws->dx, ws->du, ws->pred, ws->feasible,
+                               on_chip ? nullptr : ws->K, on_chip ? nullptr : ws->d, nullptr,
+                               nullptr, stream);
   if (rc) return rc;
   return noc_ipm_trial(fam, ws, mode, stream);
 }

@@ -20,6 +20,15 @@ struct KKTArgs {
   int lds_out; // set by the launcher: dx/du staged through LDS and written as contiguous rows
 };
 
+// On-chip staging of the KKT scan (kkt_scan_impl.h): per trajectory N slots of nu*(nx+1) doubles
+// (K_s, d_s, later overwritten by dx_s, du_s) + dx_N, one region per L-lane segment of the
+// 64-thread block.  Staged when a block's region fits in 20 KB (8 resident waves per CU).
+inline size_t kkt_lds_bytes_rt(int nx, int nu, int N, int L) {
+  const size_t per_traj = (size_t)(((long long)N * nu * (nx + 1) + nx + 1) & ~1LL);
+  const size_t bytes = (size_t)(64 / L) * per_traj * sizeof(double);
+  return bytes <= 20480 ? bytes : 0;
+}
+
 hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t stream);
 hipError_t kkt_dispatch_2x1(const KKTArgs& a, int lanes, hipStream_t stream);
 hipError_t kkt_dispatch_4x1(const KKTArgs& a, int lanes, hipStream_t stream);

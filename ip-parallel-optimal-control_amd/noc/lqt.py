@@ -28,8 +28,8 @@ class KKTResult(NamedTuple):
     du: torch.Tensor          # (Bt, N, nu)
     pred: torch.Tensor        # (Bt,)  sum of dV (noc/seq_interior_point_newton.py:63,75)
     feasible: torch.Tensor    # (Bt,) int32, all Quu > 0 (S:52-53)
-    K: torch.Tensor           # (Bt, N, nu, nx)
-    d: torch.Tensor           # (Bt, N, nu)
+    K: Optional[torch.Tensor]  # (Bt, N, nu, nx), None if want_gains=False
+    d: Optional[torch.Tensor]  # (Bt, N, nu), None if want_gains=False
     S: Optional[torch.Tensor]  # (Bt, N+1, nx, nx) or None
     v: Optional[torch.Tensor]  # (Bt, N+1, nx) or None
 
@@ -51,12 +51,19 @@ def _batched(*ts):
     return False, list(ts)
 
 
+def gains_on_chip(nx: int, nu: int, N: int, lanes: int = 0) -> bool:
+    """True if the fused solve keeps K, d in LDS (noc_kkt_gains_on_chip), so they may be omitted."""
+    return _lib.load().noc_kkt_gains_on_chip(nx, nu, N, lanes) == 1
+
+
 def kkt_solve(A, B, Q, R, M, r, P, reg=None, x0=None, q=None, c=None, p=None, active=None,
               lanes: int = 0, want_value: bool = False, out: Optional[KKTResult] = None,
-              ) -> KKTResult:
+              want_gains: bool = True) -> KKTResult:
     """Batched fused KKT solve (bwd + fwd).  Shapes (leading batch Bt optional):
     A (Bt,N,nx,nx) B (Bt,N,nx,nu) Q (Bt,N,nx,nx) R (Bt,N,nu,nu) M (Bt,N,nx,nu) r (Bt,N,nu)
-    P (Bt,nx,nx) reg (Bt,) x0/p (Bt,nx) q/c (Bt,N,nx) active (Bt,) int32."""
+    P (Bt,nx,nx) reg (Bt,) x0/p (Bt,nx) q/c (Bt,N,nx) active (Bt,) int32.
+    want_gains=False: par_Newton's outputs only (dx, du, pred, feasible); K, d are then kept on
+    chip when they fit (gains_on_chip) and returned as None."""
     squeeze, (A, B, Q, R, M, r, P, x0, q, c, p) = _batched(A, B, Q, R, M, r, P, x0, q, c, p)
     if squeeze and reg is not None and reg.dim() == 0:
         reg = reg.reshape(1)
@@ -69,10 +76,12 @@ def kkt_solve(A, B, Q, R, M, r, P, reg=None, x0=None, q=None, c=None, p=None, ac
         active = active.to(device=dev, dtype=torch.int32).contiguous()
     if out is None:
         f64 = dict(device=dev, dtype=torch.float64)
+        gains = want_gains or not gains_on_chip(nx, nu, N, lanes)
         out = KKTResult(
             torch.empty(Bt, N + 1, nx, **f64), torch.empty(Bt, N, nu, **f64),
             torch.empty(Bt, **f64), torch.empty(Bt, device=dev, dtype=torch.int32),
-            torch.empty(Bt, N, nu, nx, **f64), torch.empty(Bt, N, nu, **f64),
+            torch.empty(Bt, N, nu, nx, **f64) if gains else None,
+            torch.empty(Bt, N, nu, **f64) if gains else None,
             torch.empty(Bt, N + 1, nx, nx, **f64) if want_value else None,
             torch.empty(Bt, N + 1, nx, **f64) if want_value else None)
     lib = _lib.load()
@@ -151,18 +160,20 @@ def to_tiled(A, B, Q, R, M, r, P, lanes: int) -> TiledBlocks:
 
 
 def kkt_solve_tiled(tb: TiledBlocks, reg=None, x0=None, active=None, want_value=False,
-                    out: Optional[KKTResult] = None) -> KKTResult:
+                    out: Optional[KKTResult] = None, want_gains: bool = True) -> KKTResult:
     """Fused KKT solve on tiled blocks (the layout the interior-point workspace produces).
-    K, d of the result are flat tiled buffers; dx, du, S, v natural."""
+    K, d of the result are flat tiled buffers (None if want_gains=False and they fit on chip);
+    dx, du, S, v natural."""
     Bt, N, nx, nu, L = tb.Bt, tb.N, tb.nx, tb.nu, tb.lanes
     dev = tb.A.device
     if out is None:
         f64 = dict(device=dev, dtype=torch.float64)
+        gains = want_gains or not gains_on_chip(nx, nu, N, L)
         out = KKTResult(
             torch.empty(Bt, N + 1, nx, **f64), torch.empty(Bt, N, nu, **f64),
             torch.empty(Bt, **f64), torch.empty(Bt, device=dev, dtype=torch.int32),
-            torch.empty(tiled_numel(N, Bt, L, nu * nx), **f64),
-            torch.empty(tiled_numel(N, Bt, L, nu), **f64),
+            torch.empty(tiled_numel(N, Bt, L, nu * nx), **f64) if gains else None,
+            torch.empty(tiled_numel(N, Bt, L, nu), **f64) if gains else None,
             torch.empty(Bt, N + 1, nx, nx, **f64) if want_value else None,
             torch.empty(Bt, N + 1, nx, **f64) if want_value else None)
     if active is not None:

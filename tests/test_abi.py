@@ -43,6 +43,20 @@ def test_supported_shapes_and_lanes():
     assert lib.noc_kkt_default_lanes(4, 1, 200) in (8, 16, 32, 64)
 
 
+def test_gains_on_chip_query_and_required_workspace():
+    """K, d may be NULL only where the fused solve keeps them in LDS (20 KB per 64-lane block)."""
+    from noc import _lib
+    lib = _lib.load()
+    assert lib.noc_kkt_gains_on_chip(4, 1, 200, 32) == 1   # c3 default: 2 x 8 KB per wave
+    assert lib.noc_kkt_gains_on_chip(2, 1, 100, 64) == 1   # c2
+    assert lib.noc_kkt_gains_on_chip(8, 4, 512, 16) == 0   # c4: 147 KB of gains per trajectory
+    assert lib.noc_kkt_gains_on_chip(3, 1, 10, 0) == 0     # unsupported shape
+    # K = d = NULL with gains that do not fit: rejected before any launch
+    rc = lib.noc_kkt_solve(8, 4, 512, 4, 16, *([16] * 6), None, None, 16, None, None, None, None,
+                           16, 16, 16, 16, None, None, None, None, None)
+    assert rc < 0 and b"noc_kkt_gains_on_chip" in lib.noc_last_error()
+
+
 def test_argument_errors_are_reported_not_launched():
     from noc import _lib
     lib = _lib.load()

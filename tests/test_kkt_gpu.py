@@ -195,3 +195,23 @@ def test_cartpole_blocks_full_size_properties():
     assert relerr(du[sample].cpu(), ref["du"]) < RTOL
     assert relerr(res.pred[sample].cpu(), ref["pred"]) < RTOL
     assert bool(torch.all(res.feasible == 1))
+
+
+@pytest.mark.parametrize("nx,nu,N,lanes", [(2, 1, 100, 64), (4, 1, 200, 32), (4, 1, 200, 64),
+                                           (4, 1, 50, 8), (8, 4, 40, 64)])
+@pytest.mark.parametrize("affine", [False, True])
+def test_kkt_without_gains_matches_oracle(nx, nu, N, lanes, affine):
+    """par_Newton's outputs only (want_gains=False): K, d stay in LDS between the backward and
+    forward phases when they fit (noc_kkt_gains_on_chip), else go through the K/d workspace."""
+    from noc import lqt
+    case = rand_lq(77 + N + lanes + nx, 6, N, nx, nu, affine=affine)
+    ref = oracle_batch(case)
+    g = lambda k: dev(case.get(k))
+    res = lqt.kkt_solve(g("A"), g("B"), g("Q"), g("R"), g("M"), g("r"), g("P"), reg=g("reg"),
+                        x0=g("x0"), q=g("q"), c=g("c"), p=g("p"), lanes=lanes, want_gains=False)
+    torch.cuda.synchronize()
+    assert (res.K is None) == lqt.gains_on_chip(nx, nu, N, lanes)
+    for k in ["dx", "du", "pred"]:
+        got = getattr(res, k).cpu().numpy()
+        assert relerr(got, ref[k]) < RTOL, (k, relerr(got, ref[k]))
+    assert np.array_equal(res.feasible.cpu().numpy().astype(bool), ref["feasible"].astype(bool))

@@ -36,7 +36,7 @@ def main():
                 key = (L, layout)
                 times[key] = []
                 if layout == "tiled":
-                    fn = (lambda tb=tb, reg=blk["reg"], o=None: lqt.kkt_solve_tiled(tb, reg=reg, out=o))
+                    fn = (lambda tb=tb, reg=blk["reg"], o=None: lqt.kkt_solve_tiled(tb, reg=reg, out=o, want_gains=False))
                 else:
                     nat = blk["engine"].natural_blocks()
                     fn = (lambda nat=nat, reg=blk["reg"], L=L, o=None: lqt.kkt_solve(
