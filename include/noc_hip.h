@@ -23,7 +23,10 @@
  *   pred = sum_k d_k'Qu_k + 1/2 d_k'Quu_k d_k,  feasible = all_k Quu_k > 0
  *
  * Supported (nx, nu): (2,1) pendulum, (4,1) cart-pole, (8,4) stacked double integrators.
- * `lanes` = lanes of a wave64 per trajectory (64, 32, 16, 8); 0 = library default.
+ * `lanes` = lanes of a wave64 per trajectory (64, 32, 16, 8: parallel-in-time scan over the
+ * horizon, chunked over the lanes); 1 = horizon-sequential Riccati with the trajectory's algebra
+ * spread over an nx-lane group (work-efficient; for batches that fill the GPU by themselves,
+ * natural layout, gains through HBM); 0 = library default.
  */
 #ifndef NOC_HIP_H
 #define NOC_HIP_H

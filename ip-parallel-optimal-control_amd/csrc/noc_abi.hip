@@ -36,8 +36,8 @@ int check_dims(int nx, int nu, int N, int B, int lanes) {
                         "); supported: (2,1) (4,1) (8,4)");
   if (N < 1) return fail(-1, "horizon N must be >= 1");
   if (B < 0) return fail(-1, "batch B must be >= 0");
-  if (lanes != 0 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64)
-    return fail(-1, "lanes must be 0, 8, 16, 32 or 64");
+  if (lanes != 0 && lanes != 1 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64)
+    return fail(-1, "lanes must be 0, 1, 8, 16, 32 or 64");
   return 0;
 }
 }  // namespace
@@ -48,6 +48,7 @@ bool kkt_supported(int nx, int nu) {
 }
 
 hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t stream) {
+  if (lanes == 1) return kkt_group_dispatch(nx, nu, a, stream);
   if (nx == 2 && nu == 1) return kkt_dispatch_2x1(a, lanes, stream);
   if (nx == 4 && nu == 1) return kkt_dispatch_4x1(a, lanes, stream);
   if (nx == 8 && nu == 4) return kkt_dispatch_8x4(a, lanes, stream);
@@ -117,6 +118,7 @@ static int kkt_common(int mode, int tiled, int nx, int nu, int N, int B, int lan
   a.ablate = g_ablate;
   a.tiled = tiled;
   if (tiled && lanes == 0) return fail(-1, "the tiled layout needs an explicit lanes value");
+  if (tiled && lanes == 1) return fail(-1, "lanes = 1 (group solve) reads the natural layout");
   (void)bwd;
   (void)fwd;
   const int L = lanes ? lanes : noc::kkt_default_lanes(nx, nu, N);

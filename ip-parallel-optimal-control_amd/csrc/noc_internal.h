@@ -24,12 +24,15 @@ struct KKTArgs {
 // (K_s, d_s, later overwritten by dx_s, du_s) + dx_N, one region per L-lane segment of the
 // 64-thread block.  Staged when a block's region fits in 20 KB (8 resident waves per CU).
 inline size_t kkt_lds_bytes_rt(int nx, int nu, int N, int L) {
+  if (L < 8) return 0;  // lanes = 1 (group solve): gains go through HBM
   const size_t per_traj = (size_t)(((long long)N * nu * (nx + 1) + nx + 1) & ~1LL);
   const size_t bytes = (size_t)(64 / L) * per_traj * sizeof(double);
   return bytes <= 20480 ? bytes : 0;
 }
 
 hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t stream);
+// lanes == 1: horizon-sequential solve, one trajectory per nx-lane group (kkt_group_impl.h)
+hipError_t kkt_group_dispatch(int nx, int nu, const KKTArgs& a, hipStream_t stream);
 hipError_t kkt_dispatch_2x1(const KKTArgs& a, int lanes, hipStream_t stream);
 hipError_t kkt_dispatch_4x1(const KKTArgs& a, int lanes, hipStream_t stream);
 hipError_t kkt_dispatch_8x4(const KKTArgs& a, int lanes, hipStream_t stream);

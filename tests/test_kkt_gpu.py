@@ -37,10 +37,11 @@ def run_kkt(case, lanes, want_value=True):
 
 
 @pytest.mark.parametrize("nx,nu", [(2, 1), (4, 1), (8, 4)])
-@pytest.mark.parametrize("lanes", [64, 32, 16, 8])
+@pytest.mark.parametrize("lanes", [64, 32, 16, 8, 1])
 @pytest.mark.parametrize("N", [1, 7, 50, 200])
 @pytest.mark.parametrize("affine", [False, True])
 def test_kkt_matches_oracle(nx, nu, lanes, N, affine):
+    """lanes 64..8: parallel-in-time scan; lanes 1: horizon-sequential nx-lane group solve."""
     case = rand_lq(1000 * nx + N + lanes + int(affine), 5, N, nx, nu, affine=affine)
     ref = oracle_batch(case)
     out = run_kkt(case, lanes)
@@ -62,7 +63,8 @@ def test_kkt_infeasible_flag():
     assert relerr(out["dx"][ok], ref["dx"][ok]) < RTOL
 
 
-def test_kkt_active_mask_leaves_inactive_untouched():
+@pytest.mark.parametrize("lanes", [0, 1])
+def test_kkt_active_mask_leaves_inactive_untouched(lanes):
     from noc import lqt
     case = rand_lq(11, 6, 40, 4, 1)
     g = lambda k: dev(case.get(k))
@@ -74,7 +76,7 @@ def test_kkt_active_mask_leaves_inactive_untouched():
                         torch.zeros(Bt, N, 1, dtype=torch.float64, device="cuda"), None, None)
     active = torch.tensor([1, 0, 1, 0, 0, 1], dtype=torch.int32, device="cuda")
     lqt.kkt_solve(g("A"), g("B"), g("Q"), g("R"), g("M"), g("r"), g("P"), reg=g("reg"),
-                  active=active, out=out)
+                  active=active, out=out, lanes=lanes)
     torch.cuda.synchronize()
     ref = oracle_batch(case)
     dx = out.dx.cpu().numpy()
@@ -86,14 +88,17 @@ def test_kkt_active_mask_leaves_inactive_untouched():
 
 
 @pytest.mark.parametrize("nx,nu", [(2, 1), (4, 1), (8, 4)])
-def test_split_bwd_fwd_entry_points(nx, nu):
+@pytest.mark.parametrize("bwd_lanes,fwd_lanes", [(16, 32), (1, 1), (1, 64), (8, 1)])
+def test_split_bwd_fwd_entry_points(nx, nu, bwd_lanes, fwd_lanes):
+    """par_bwd_pass / par_fwd_pass split; the scan and the group solve interoperate through K, d."""
     from noc import lqt
     case = rand_lq(5 + nx, 3, 37, nx, nu, affine=True)
     g = lambda k: dev(case.get(k))
     ref = oracle_batch(case)
     K, d, S, v, pred, feas = lqt.bwd_pass(g("A"), g("B"), g("Q"), g("R"), g("M"), g("r"), g("P"),
-                                          reg=g("reg"), q=g("q"), c=g("c"), p=g("p"), lanes=16)
-    du, dx = lqt.fwd_pass(g("A"), g("B"), K, d, x0=g("x0"), c=g("c"), lanes=32)
+                                          reg=g("reg"), q=g("q"), c=g("c"), p=g("p"),
+                                          lanes=bwd_lanes)
+    du, dx = lqt.fwd_pass(g("A"), g("B"), K, d, x0=g("x0"), c=g("c"), lanes=fwd_lanes)
     torch.cuda.synchronize()
     assert relerr(K.cpu(), ref["K"]) < RTOL
     assert relerr(S.cpu(), ref["S"]) < RTOL
@@ -215,3 +220,29 @@ def test_kkt_without_gains_matches_oracle(nx, nu, N, lanes, affine):
         got = getattr(res, k).cpu().numpy()
         assert relerr(got, ref[k]) < RTOL, (k, relerr(got, ref[k]))
     assert np.array_equal(res.feasible.cpu().numpy().astype(bool), ref["feasible"].astype(bool))
+
+
+def test_group_solve_linear8_blocks_properties():
+    """c4 family (four stacked RK4 double integrators, nx=8, nu=4) at N=512 with a reduced batch:
+    the horizon-sequential group solve (lanes=1) against the oracle on a sample, dynamics
+    consistency on every trajectory, and agreement with the parallel scan (lanes=16)."""
+    from noc import lqt
+    from noc.problems import make_bench_blocks
+    blocks = make_bench_blocks("linear8", N=512, batch=512, seed=3, natural=True)
+    nat = [blocks[k] for k in ("A", "B", "Q", "R", "M", "r", "P")]
+    res = lqt.kkt_solve(*nat, reg=blocks["reg"], lanes=1)
+    scan = lqt.kkt_solve(*nat, reg=blocks["reg"], lanes=16)
+    torch.cuda.synchronize()
+    dx, du = res.dx, res.du
+    pred_dx = torch.einsum("bkij,bkj->bki", blocks["A"], dx[:, :-1]) + \
+        torch.einsum("bkij,bkj->bki", blocks["B"], du)
+    scale = max(1.0, dx.abs().max().item())
+    assert (pred_dx - dx[:, 1:]).abs().max().item() <= 1e-12 * scale
+    assert (scan.dx - dx).abs().max().item() <= 1e-9 * scale
+    sample = list(range(0, 512, 64))
+    case = {k: blocks[k][sample].cpu().numpy() for k in ["A", "B", "Q", "R", "M", "r", "P", "reg"]}
+    ref = oracle_batch(case)
+    assert relerr(dx[sample].cpu(), ref["dx"]) < RTOL
+    assert relerr(du[sample].cpu(), ref["du"]) < RTOL
+    assert relerr(res.pred[sample].cpu(), ref["pred"]) < RTOL
+    assert bool(torch.all(res.feasible == 1))

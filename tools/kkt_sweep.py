@@ -29,10 +29,11 @@ def main():
         name, N, B = CONFIGS[cname]
         times, outs, tbs = {}, {}, {}
         for L in [int(x) for x in args.lanes.split(",")]:
-            blk = problems.make_bench_blocks(name, N=N, batch=B, seed=7, lanes=L)
+            # lanes = 1 (horizon-sequential group solve) reads the natural layout only
+            blk = problems.make_bench_blocks(name, N=N, batch=B, seed=7, lanes=L if L > 1 else 16)
             tb = blk["tiled"]
             nx, nu = tb.nx, tb.nu
-            for layout in args.layouts.split(","):
+            for layout in (args.layouts.split(",") if L > 1 else ["natural"]):
                 key = (L, layout)
                 times[key] = []
                 if layout == "tiled":
@@ -40,7 +41,8 @@ def main():
                 else:
                     nat = blk["engine"].natural_blocks()
                     fn = (lambda nat=nat, reg=blk["reg"], L=L, o=None: lqt.kkt_solve(
-                        *(nat[k] for k in ("A", "B", "Q", "R", "M", "r", "P")), reg=reg, lanes=L, out=o))
+                        *(nat[k] for k in ("A", "B", "Q", "R", "M", "r", "P")), reg=reg, lanes=L,
+                        out=o, want_gains=False))
                 outs[key] = fn()
                 tbs[key] = fn
             del blk
