@@ -24,6 +24,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ip-parallel-optimal-control_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+CONFIG_LABEL = {("cartpole", 200, 4096): "BASELINE c3; c5 when run on 8 GPUs",
+                ("pendulum", 100, 1024): "BASELINE c2",
+                ("linear8", 512, 16384): "BASELINE c4"}
 
 
 def algorithmic_bytes(nx, nu, N, B):
@@ -43,7 +46,7 @@ def pmc_traffic(path, kernel_substr):
         return None
 
 
-def cpu_baseline(blocks, sample, seconds=10.0):
+def cpu_baseline(blocks, sample, seconds=10.0, problem="cartpole"):
     """Time the C restatement of the sequential KKT solve on `sample` trajectories (the same
     blocks, relaid out to the natural layout)."""
     sys.path.insert(0, ROOT)
@@ -54,15 +57,33 @@ def cpu_baseline(blocks, sample, seconds=10.0):
     del nat
     cores = len(os.sched_getaffinity(0))
     cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
-    kkt_ref.solve(*(host[k] for k in ("A", "B", "Q", "R", "M", "r", "P", "reg")), threads=cores)
+    ref = kkt_ref.solve(*(host[k] for k in ("A", "B", "Q", "R", "M", "r", "P", "reg")),
+                        threads=cores)
     reps, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         kkt_ref.solve(*(host[k] for k in ("A", "B", "Q", "R", "M", "r", "P", "reg")), threads=cores)
         reps += 1
     dt = time.perf_counter() - t0
     return dict(value=reps * sample / dt, unit="trajectory-KKT-steps/s", cores=cores, kind="port",
-                sample=f"{sample} cart-pole trajectories x N={host['A'].shape[1]}, {reps} repeats "
-                       f"({dt:.1f} s) of the OpenMP C sequential Riccati (oracle/kkt_ref.c)")
+                sample=f"{sample} {problem} trajectories x N={host['A'].shape[1]}, {reps} repeats "
+                       f"({dt:.1f} s) of the OpenMP C sequential Riccati (oracle/kkt_ref.c)"), ref
+
+
+def residual_vs_seq_ref(out, ref, sample):
+    """BASELINE metric's 'fp64 residual vs seq ref': max relative deviation of the GPU step from
+    the sequential-Riccati restatement (oracle/kkt_ref.c) on the sampled trajectories."""
+    import numpy as np
+    res = {}
+    for k in ("dx", "du", "pred"):
+        got = getattr(out, k)[:sample].double().cpu().numpy()
+        want = ref[k]
+        res[k] = float(np.max(np.abs(got - want)) / max(1.0, float(np.max(np.abs(want)))))
+    res["feasible_equal"] = bool(np.array_equal(out.feasible[:sample].cpu().numpy(),
+                                                ref["feasible"]))
+    res["max"] = max(res["dx"], res["du"], res["pred"])
+    res["tolerance"] = 1e-10
+    res["sample"] = sample
+    return res
 
 
 def main():
@@ -93,10 +114,14 @@ def main():
     from noc import lqt, problems, _lib
 
     N, B = args.horizon, args.batch
+    if args.lanes == 1:  # horizon-sequential group solve: natural layout only
+        args.layout = "natural"
     blocks = problems.make_bench_blocks(args.problem, N=N, batch=B, seed=1234 + rank,
-                                        lanes=args.lanes, natural=(args.layout == "natural"))
+                                        lanes=args.lanes if args.lanes != 1 else 16,
+                                        natural=(args.layout == "natural"))
     tb = blocks["tiled"]
-    nx, nu, lanes = tb.nx, tb.nu, tb.lanes
+    nx, nu = tb.nx, tb.nu
+    lanes = args.lanes if args.lanes == 1 else tb.lanes
     if args.layout == "tiled":
         out = lqt.kkt_solve_tiled(tb, reg=blocks["reg"], want_gains=False)
 
@@ -149,10 +174,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: first Newton iterate (bp=0.1) of random-start cart-pole problems, "
-                "linearised on device",
+        "data": f"synthetic: first Newton iterate (bp=0.1) of random-start {args.problem} "
+                "problems, linearised on device",
         "config": {"workload": f"{args.problem} nx={nx} nu={nu} N={N} batch={B}/GPU "
-                               f"(BASELINE c3; c5 when run on 8 GPUs)",
+                               f"({CONFIG_LABEL.get((args.problem, N, B), 'custom')})",
                    "layout": args.layout,
                    "horizon": N, "batch_per_gpu": B, "global_batch": B * world,
                    "lanes_per_trajectory": lanes, "parallelism": f"trajectory-sharded x{world}"},
@@ -163,7 +188,10 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
-            result["cpu_baseline"] = cpu_baseline(blocks, min(args.cpu_sample, B), args.cpu_seconds)
+            sample = min(args.cpu_sample, B)
+            result["cpu_baseline"], ref = cpu_baseline(blocks, sample, args.cpu_seconds,
+                                                             args.problem)
+            result["residual_vs_seq_ref"] = residual_vs_seq_ref(out, ref, sample)
         except Exception as e:  # reported, never fatal
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:

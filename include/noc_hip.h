@@ -171,6 +171,17 @@ int noc_ipm_step_main(const noc_family* fam, const noc_ipm_ws* ws, int mode, int
                       void* stream);
 int noc_ipm_promote(const noc_ipm_ws* ws, void* stream);
 
+/* Persistent solve: the WHOLE barrier schedule (rollout, Newton / retry loops, barrier updates)
+ * of every trajectory in ONE launch, one wave64 per trajectory running its own reference control
+ * flow back to back (no per-step launches, no host polls, no lockstep across trajectories).
+ * Same arithmetic and results as the noc_ipm_init + noc_ipm_step loop at lanes = 64.  Requires
+ * ws->lanes == 64 and a KKT step that fits in LDS (noc_ipm_solve_supported).  A trajectory that
+ * reaches max_solves KKT solves stops with phase != NOC_PHASE_DONE.  On return (stream order)
+ * u, x, bp, rp, r_inc, cost, hu, it, total_it, kkt_solves and phase hold the final state. */
+int noc_ipm_solve_supported(const noc_family* fam, int N, int lanes);
+int noc_ipm_solve(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, double bp0,
+                  int max_solves, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,131 +16,11 @@
 #include <cmath>
 
 #include "../../include/noc_hip.h"
-#include "families_gen.h"
+#include "ipm_family.h"
 #include "noc_internal.h"
 #include "small_linalg.h"
 
 namespace noc {
-
-constexpr double kTwoPi = 6.283185307179586;  // 2.0 * jnp.pi
-
-// noc/utils.py:8-10 with jnp.remainder semantics (C fmod, + divisor if the sign differs)
-NOC_DEV double wrap_angle(double a) {
-  double r = fmod(a, kTwoPi);
-  return (r != 0.0 && r < 0.0) ? r + kTwoPi : r;
-}
-
-template <int KIND, int NX, int NU>
-struct Fam {
-  const noc_family& p;
-  NOC_DEV explicit Fam(const noc_family& prm) : p(prm) {}
-
-  // ------------------------------------------------------------------ dynamics
-  NOC_DEV void step(const double* x, const double* u, double* xn) const {
-    if constexpr (KIND == NOC_FAMILY_LINEAR) {
-      NOC_UNROLL for (int i = 0; i < NX; ++i) {
-        double t = 0.0;
-        NOC_UNROLL for (int k = 0; k < NX; ++k) t += p.A[i * NX + k] * x[k];
-        NOC_UNROLL for (int j = 0; j < NU; ++j) t += p.B[i * NU + j] * u[j];
-        xn[i] = t;
-      }
-    } else {
-      double f[NX];
-      if constexpr (KIND == NOC_FAMILY_PENDULUM) gen::pendulum_ode(x, u, f);
-      else gen::cartpole_ode(x, u, f);
-      NOC_UNROLL for (int i = 0; i < NX; ++i) xn[i] = x[i] + p.dt * f[i];  // noc/utils.py:50-54
-    }
-  }
-  NOC_DEV void jac(const double* x, const double* u, double* fx, double* fu) const {
-    if constexpr (KIND == NOC_FAMILY_LINEAR) {
-      NOC_UNROLL for (int i = 0; i < NX * NX; ++i) fx[i] = p.A[i];
-      NOC_UNROLL for (int i = 0; i < NX * NU; ++i) fu[i] = p.B[i];
-    } else {
-      constexpr int NZ = NX + NU;
-      double J[NX * NZ];
-      if constexpr (KIND == NOC_FAMILY_PENDULUM) gen::pendulum_ode_jac(x, u, J);
-      else gen::cartpole_ode_jac(x, u, J);
-      NOC_UNROLL for (int i = 0; i < NX; ++i) {
-        NOC_UNROLL for (int j = 0; j < NX; ++j) fx[i * NX + j] = (i == j ? 1.0 : 0.0) + p.dt * J[i * NZ + j];
-        NOC_UNROLL for (int j = 0; j < NU; ++j) fu[i * NU + j] = p.dt * J[i * NZ + NX + j];
-      }
-    }
-  }
-  // sum_i lam_i d2 f_i (Euler: dt * ode Hessians); adds into Hxx (NXxNX), Huu, Hxu (NXxNU)
-  NOC_DEV void add_hess_l(const double* x, const double* u, const double* lam, double* Hxx,
-                          double* Huu, double* Hxu) const {
-    if constexpr (KIND != NOC_FAMILY_LINEAR) {
-      constexpr int NZ = NX + NU;
-      double H[NZ * NZ];
-      if constexpr (KIND == NOC_FAMILY_PENDULUM) gen::pendulum_ode_hess_l(x, u, lam, H);
-      else gen::cartpole_ode_hess_l(x, u, lam, H);
-      NOC_UNROLL for (int i = 0; i < NX; ++i) {
-        NOC_UNROLL for (int j = 0; j < NX; ++j) Hxx[i * NX + j] += p.dt * H[i * NZ + j];
-        NOC_UNROLL for (int j = 0; j < NU; ++j) Hxu[i * NU + j] += p.dt * H[i * NZ + NX + j];
-      }
-      NOC_UNROLL for (int i = 0; i < NU; ++i)
-        NOC_UNROLL for (int j = 0; j < NU; ++j) Huu[i * NU + j] += p.dt * H[(NX + i) * NZ + NX + j];
-    }
-  }
-
-  // ------------------------------------------------------------------ costs
-  NOC_DEV double err(const double* x, int i) const {
-    const double xi = (i == p.wrap_index) ? wrap_angle(x[i]) : x[i];
-    return xi - p.goal[i];
-  }
-  NOC_DEV bool barrier() const { return p.u_bound > 0.0; }
-  // stage cost (PR:40-50 / CR:36-45 / LD:138-141)
-  NOC_DEV double stage_cost(const double* x, const double* u, double bp) const {
-    double c = 0.0;
-    NOC_UNROLL for (int i = 0; i < NX; ++i) { const double e = err(x, i); c += p.wx[i] * e * e; }
-    c *= 0.5;
-    double cu = 0.0;
-    NOC_UNROLL for (int j = 0; j < NU; ++j) cu += p.wu[j] * u[j] * u[j];
-    c += 0.5 * cu;
-    if (barrier()) {
-      double lb = 0.0;
-      NOC_UNROLL for (int j = 0; j < NU; ++j) lb += log(p.u_bound - u[j]) + log(u[j] + p.u_bound);
-      c -= bp * lb;
-    }
-    return c;
-  }
-  NOC_DEV void stage_grad(const double* x, const double* u, double bp, double* cx,
-                          double* cu) const {
-    NOC_UNROLL for (int i = 0; i < NX; ++i) cx[i] = p.wx[i] * err(x, i);
-    NOC_UNROLL for (int j = 0; j < NU; ++j) {
-      double g = p.wu[j] * u[j];
-      if (barrier()) g += bp / (p.u_bound - u[j]) - bp / (u[j] + p.u_bound);
-      cu[j] = g;
-    }
-  }
-  NOC_DEV double stage_cuu(const double* u, double bp, int j) const {
-    double h = p.wu[j];
-    if (barrier()) {
-      const double a = p.u_bound - u[j], b = u[j] + p.u_bound;
-      h += bp / (a * a) + bp / (b * b);
-    }
-    return h;
-  }
-  NOC_DEV bool feasible(const double* u) const {  // all(constraints <= 0) (P:45-47)
-    if (!barrier()) return true;
-    bool ok = true;
-    NOC_UNROLL for (int j = 0; j < NU; ++j) ok = ok && (u[j] - p.u_bound <= 0.0) && (-u[j] - p.u_bound <= 0.0);
-    return ok;
-  }
-  NOC_DEV double final_cost(const double* x) const {
-    double c = 0.0;
-    NOC_UNROLL for (int i = 0; i < NX; ++i) { const double e = err(x, i); c += p.wf[i] * e * e; }
-    return 0.5 * c;
-  }
-};
-
-// ------------------------------------------------------------------------------------------------
-NOC_DEV double readlane_d(double v, int lane) {  // wave-uniform broadcast of one lane's double
-  const long long bits = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), lane);
-  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), lane);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 
 // Rollout x_{k+1} = f(x_k, u_k) (noc/utils.py:57-63), one wave64 per trajectory.  The recurrence
 // is inherently sequential; every lane evaluates it redundantly (free in SIMD) with u_k broadcast
@@ -392,10 +272,6 @@ __global__ __launch_bounds__(256) void mark_solve_kernel(noc_ipm_ws w) {
 
 // ------------------------------------------------------------------------------------------------
 // trial point + Newton / barrier logic: one wave64 per trajectory (4 per 256-thread block)
-NOC_DEV double wave_sum(double v) {
-  NOC_UNROLL for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
 
 template <int KIND, int NX, int NU>
 __global__ __launch_bounds__(256) void trial_kernel(noc_family prm, noc_ipm_ws w, int mode) {

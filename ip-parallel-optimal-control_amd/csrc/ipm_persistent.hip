@@ -1,0 +1,385 @@
+// Persistent batched interior-point solver: the WHOLE barrier schedule of one trajectory in one
+// wave64, one launch for the batch (fp64, gfx950).
+//
+// Replaces par_interior_point_optimal_control / newton_oc (noc/par_interior_point_newton.py:
+// 127-254) and, with NOC_MODE_SEQ, seq_interior_point_optimal_control (noc/seq_interior_point_
+// newton.py:108-202), for registered families.  Every trajectory runs its own reference control
+// flow back to back -- rollout, linearise, costates, LQ blocks, KKT scan, trial / accept /
+// regularisation, Newton stop test, barrier schedule -- with no kernel boundary, no host poll and
+// no all-trajectory lockstep: a trajectory that needs 850 Newton steps no longer holds 4095 others
+// in per-step launches, and the per-step launch overhead is gone.
+//
+// Same arithmetic and state machine as the multi-launch driver (ipm_kernels.hip + the KKT scan
+// kernel at lanes = 64), so both produce identical iterates.  Lane l owns the horizon chunk of
+// the tiled layout (workspace lanes must be 64); cross-lane data moves through shuffles, the
+// KKT step stays in LDS (kkt_scan_wave with lds_out and dx = du = NULL), and the few hand-offs
+// through the workspace (rollout states, pred / feasible, the terminal Hessian) are ordered by a
+// workgroup fence (one wave = one workgroup).
+#include <hip/hip_runtime.h>
+
+#include "../../include/noc_hip.h"
+#include "ipm_family.h"
+#include "kkt_scan_impl.h"
+#include "noc_internal.h"
+
+namespace noc {
+
+namespace {
+constexpr int PL = 64;  // lanes per trajectory in the persistent solver
+
+NOC_DEV void wave_fence() { __threadfence_block(); }
+
+// Wave-uniform solver state, parked in LDS across the KKT scan (whose register footprint is the
+// kernel's peak) instead of being kept live in VGPRs through it.
+struct IpmState {
+  double bp, rp, rinc, cost, hu, gnorm;
+  int it, inner, total_it, solves;
+};
+template <int NX, int NU>
+NOC_DEV IpmState* state_slot(int N) {
+  extern __shared__ __attribute__((aligned(16))) double noc_smem[];
+  return reinterpret_cast<IpmState*>(noc_smem + ((N * kd_width<NX, NU>() + NX + 1) & ~1));
+}
+}  // namespace
+
+template <int KIND, int NX, int NU>
+__global__ __launch_bounds__(64, 2) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
+                                                         int terminal, double bp0,
+                                                         int max_solves) {
+  const int b = blockIdx.x;  // one wave (= one 64-thread workgroup) per trajectory
+  const int l = threadIdx.x;
+  if (b >= w.Bt) return;
+  constexpr int KD = kd_width<NX, NU>();
+  Fam<KIND, NX, NU> f(prm);
+  const int N = w.N;
+  const Chunks ch(N, PL);
+  const int start = ch.start(l), len = ch.len(l), cmax = ch.cmax;
+  const bool last = (l == PL - 1);
+  double* X = w.x + (size_t)b * (N + 1) * NX;
+  double* U = w.u + (size_t)b * N * NU;
+  double* LAM = w.lam + (size_t)b * (N + 1) * NX;
+  const double* slot = lds_slots<NX, NU, PL>(N);
+
+  KKTArgs a{};
+  a.N = N;
+  a.B = w.Bt;
+  a.mode = MODE_FULL;
+  a.A = w.A; a.Bm = w.B; a.Q = w.Q; a.R = w.R; a.M = w.M; a.r = w.r; a.P = w.P; a.reg = w.reg;
+  a.pred = w.pred; a.feasible = w.feasible;
+  a.tiled = 1;
+  a.lds_out = 1;  // dx, du stay in LDS (a.dx = a.du = NULL): the trial reads them there
+
+  double bp = bp0, rp = 1.0, rinc = 2.0, cost = 0.0, hu = 1.0, gnorm = 0.0;
+  int it = 0, inner = 0, total_it = 0, solves = 0;
+  bool capped = false;
+
+  for (;;) {  // ---------------- barrier stages (P:228-254) ----------------
+    // rollout x_{k+1} = f(x_k, u_k) (noc/utils.py:57-63, P:133): every lane runs the recurrence
+    // redundantly with u_k broadcast by readlane; lane t stores the states of block step t
+    wave_fence();  // u was last written chunk-wise by the trials
+    {
+      double x[NX];
+      NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = w.x0[(size_t)b * NX + i];
+      if (l < NX) X[l] = x[l];
+      for (int base = 0; base < N; base += 64) {
+        const int k = base + l;
+        double uk[NU];
+        NOC_UNROLL for (int j = 0; j < NU; ++j) uk[j] = (k < N) ? U[(size_t)k * NU + j] : 0.0;
+        double mine[NX];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) mine[i] = 0.0;
+        const int cnt = (N - base < 64) ? (N - base) : 64;
+        for (int t = 0; t < cnt; ++t) {
+          double ut[NU], xn[NX];
+          NOC_UNROLL for (int j = 0; j < NU; ++j) ut[j] = readlane_d(uk[j], t);
+          f.step(x, ut, xn);
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            x[i] = xn[i];
+            mine[i] = (l == t) ? xn[i] : mine[i];
+          }
+        }
+        if (k < N) NOC_UNROLL for (int i = 0; i < NX; ++i) X[(size_t)(k + 1) * NX + i] = mine[i];
+      }
+    }
+    wave_fence();  // states of every stage visible to their chunk owners
+    bool relinearize = true;
+    bool stage_done = false;
+    while (!stage_done) {  // ---------------- Newton iterations (P:127-225) ----------------
+      if (relinearize) {
+        // linearise the own chunk (P:13-28): A = fx, B = fu, cx, cu, stage cost
+        for (int j = 0; j < len; ++j) {
+          const int k = start + j;
+          double x[NX], u[NU];
+          gload<NX>(X + (size_t)k * NX, x);
+          NOC_UNROLL for (int i = 0; i < NU; ++i) u[i] = U[(size_t)k * NU + i];
+          double fx[NX * NX], fu[NX * NU], cx[NX], cu[NU];
+          f.jac(x, u, fx, fu);
+          f.stage_grad(x, u, bp, cx, cu);
+          tstore<NX * NX, PL>(w.A, b, j, l, cmax, fx);
+          tstore<NX * NU, PL>(w.B, b, j, l, cmax, fu);
+          tstore<NX, PL>(w.cx, b, j, l, cmax, cx);
+          tstore<NU, PL>(w.cu, b, j, l, cmax, cu);
+          const double lc = f.stage_cost(x, u, bp);
+          tstore<1, PL>(w.lc, b, j, l, cmax, &lc);
+        }
+        // costates as a reverse affine scan (C:34-54) fused with the LQ blocks (P:31-42)
+        const double* xN = X + (size_t)N * NX;
+        double lamN[NX];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) lamN[i] = prm.wf[i] * f.err(xN, i);
+        Mat<NX, NX> G;
+        Vec<NX> g;
+        set_identity(G);
+        set_zero(g);
+        for (int j = len - 1; j >= 0; --j) {
+          double A[NX * NX], cx[NX];
+          tload<NX * NX, PL>(w.A, b, j, l, cmax, A);
+          tload<NX, PL>(w.cx, b, j, l, cmax, cx);
+          Mat<NX, NX> Gn;
+          Vec<NX> gn;
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            double t = cx[i];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) t += A[m * NX + i] * g[m];
+            gn[i] = t;
+            NOC_UNROLL for (int jj = 0; jj < NX; ++jj) {
+              double u = 0.0;
+              NOC_UNROLL for (int m = 0; m < NX; ++m) u += A[m * NX + i] * G(m, jj);
+              Gn(i, jj) = u;
+            }
+          }
+          G = Gn;
+          g = gn;
+        }
+        if (last) {
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            double t = g[i];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) t += G(i, m) * lamN[m];
+            g[i] = t;
+          }
+          set_zero(G);
+        }
+#pragma unroll 1
+        for (int d = 1; d < PL; d <<= 1) {
+          Mat<NX, NX> G2;
+          Vec<NX> g2;
+          shfl_down_arr<NX * NX>(G.v, G2.v, d, PL);
+          shfl_down_arr<NX>(g.v, g2.v, d, PL);
+          Mat<NX, NX> Gn;
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            double t = g[i];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) t += G(i, m) * g2[m];
+            g[i] = t;
+            NOC_UNROLL for (int jj = 0; jj < NX; ++jj) {
+              double u = 0.0;
+              NOC_UNROLL for (int m = 0; m < NX; ++m) u += G(i, m) * G2(m, jj);
+              Gn(i, jj) = u;
+            }
+          }
+          G = Gn;
+        }
+        double lam[NX];
+        shfl_down_arr<NX>(g.v, lam, 1, PL);
+        if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = lamN[i];
+        if (last) gstore<NX>(LAM + (size_t)N * NX, lamN);
+        double csum = 0.0, hmax = 0.0, g2s = 0.0;
+        for (int j = len - 1; j >= 0; --j) {
+          const int k = start + j;
+          double A[NX * NX], Bm[NX * NU], cx[NX], cu[NU], lc, rr[NU];
+          tload<NX * NX, PL>(w.A, b, j, l, cmax, A);
+          tload<NX * NU, PL>(w.B, b, j, l, cmax, Bm);
+          tload<NX, PL>(w.cx, b, j, l, cmax, cx);
+          tload<NU, PL>(w.cu, b, j, l, cmax, cu);
+          tload<1, PL>(w.lc, b, j, l, cmax, &lc);
+          // LQ blocks at lambda_{k+1} (P:35-37): Q = cxx + l.fxx, R = cuu + l.fuu, M = cxu + l.fxu
+          {
+            double x[NX], u[NU];
+            gload<NX>(X + (size_t)k * NX, x);
+            NOC_UNROLL for (int i = 0; i < NU; ++i) u[i] = U[(size_t)k * NU + i];
+            double Q[NX * NX], R[NU * NU], M[NX * NU];
+            NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int jj = 0; jj < NX; ++jj) Q[i * NX + jj] = (i == jj) ? prm.wx[i] : 0.0;
+            NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int jj = 0; jj < NU; ++jj) R[i * NU + jj] = (i == jj) ? f.stage_cuu(u, bp, i) : 0.0;
+            NOC_UNROLL for (int i = 0; i < NX * NU; ++i) M[i] = 0.0;
+            f.add_hess_l(x, u, lam, Q, R, M);
+            Sym<NX> Qs;
+            Sym<NU> Rs;
+            NOC_UNROLL for (int i = 0; i < NX; ++i)
+              NOC_UNROLL for (int jj = i; jj < NX; ++jj) Qs(i, jj) = (i == jj) ? Q[i * NX + i] : 0.5 * (Q[i * NX + jj] + Q[jj * NX + i]);
+            NOC_UNROLL for (int i = 0; i < NU; ++i)
+              NOC_UNROLL for (int jj = i; jj < NU; ++jj) Rs(i, jj) = (i == jj) ? R[i * NU + i] : 0.5 * (R[i * NU + jj] + R[jj * NU + i]);
+            tstore<Sym<NX>::SZ, PL>(w.Q, b, j, l, cmax, Qs.v);
+            tstore<Sym<NU>::SZ, PL>(w.R, b, j, l, cmax, Rs.v);
+            tstore<NX * NU, PL>(w.M, b, j, l, cmax, M);
+            if (terminal == NOC_TERMINAL_STAGE0 && k == 0) gstore<NX * NX>(w.P + (size_t)b * NX * NX, Q);  // P:73
+          }
+          NOC_UNROLL for (int jj = 0; jj < NU; ++jj) {  // ru_k = cu_k + fu_k' lambda_{k+1}  (P:34)
+            double r = cu[jj];
+            NOC_UNROLL for (int i = 0; i < NX; ++i) r += Bm[i * NU + jj] * lam[i];
+            rr[jj] = r;
+            hmax = fmax(hmax, fabs(r));
+            g2s += cu[jj] * cu[jj];
+          }
+          tstore<NU, PL>(w.r, b, j, l, cmax, rr);
+          double ln[NX];
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            double t = cx[i];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) t += A[m * NX + i] * lam[m];
+            ln[i] = t;
+          }
+          NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = ln[i];
+          gstore<NX>(LAM + (size_t)k * NX, lam);
+          csum += lc;
+        }
+        NOC_UNROLL for (int off = PL / 2; off > 0; off >>= 1) {
+          csum += __shfl_xor(csum, off, PL);
+          g2s += __shfl_xor(g2s, off, PL);
+          hmax = fmax(hmax, __shfl_xor(hmax, off, PL));
+        }
+        if (terminal == NOC_TERMINAL_FINAL_COST && last) {  // hessian(final_cost) (S:66)
+          double P[NX * NX];
+          NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int jj = 0; jj < NX; ++jj) P[i * NX + jj] = (i == jj) ? prm.wf[i] : 0.0;
+          gstore<NX * NX>(w.P + (size_t)b * NX * NX, P);
+        }
+        // total_cost(x, u, bp) (P:142); x_N is the last lane's own (trial) store
+        cost = readlane_d(csum + f.final_cost(xN), PL - 1);
+        hu = hmax;                                        // max |Hu| (P:158)
+        gnorm = sqrt(g2s);                                // ||cu||_F (P:116)
+        inner = 0;
+        // regularisation: par R += rp*||cu||*I (P:116-118); seq Quu += mu*I (S:51)
+        const double reg = (mode == NOC_MODE_PAR) ? rp * gnorm : rp;
+        w.reg[b] = reg;  // every lane stores the same value and reads its own store back
+        relinearize = false;
+      } else {
+        w.reg[b] = (mode == NOC_MODE_PAR) ? rp * gnorm : rp;
+      }
+      wave_fence();  // the terminal Hessian (stage-0 lane) and the blocks before the scan
+      {  // park the state (every lane stores the same values)
+        IpmState* st = state_slot<NX, NU>(N);
+        st->bp = bp; st->rp = rp; st->rinc = rinc; st->cost = cost; st->hu = hu; st->gnorm = gnorm;
+        st->it = it; st->inner = inner; st->total_it = total_it; st->solves = solves;
+      }
+      // ---------------- KKT solve (par_Newton, P:107-124) ----------------
+#ifndef NOC_EXPT_NOKKT
+      kkt_scan_wave<NX, NU, PL, false, true>(a, b, l);
+#endif
+      wave_fence();  // pred / feasible written by lane 0
+      {
+        const IpmState* st = state_slot<NX, NU>(N);
+        bp = st->bp; rp = st->rp; rinc = st->rinc; cost = st->cost; hu = st->hu; gnorm = st->gnorm;
+        it = st->it; inner = st->inner; total_it = st->total_it; solves = st->solves;
+      }
+      const double pred = w.pred[b];
+      const bool bwd_ok = w.feasible[b] != 0;
+      // ---------------- trial point (P:156-175 / S:121-161) ----------------
+      double tsum = 0.0;
+      int ok = 1;
+      for (int j = 0; j < len; ++j) {
+        const int k = start + j;
+        double xt[NX], ut[NU];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) xt[i] = X[(size_t)k * NX + i] + slot[k * KD + i];
+        NOC_UNROLL for (int jj = 0; jj < NU; ++jj) ut[jj] = U[(size_t)k * NU + jj] + slot[k * KD + NX + jj];
+        ok &= f.feasible(ut) ? 1 : 0;
+        tsum += f.stage_cost(xt, ut, bp);
+      }
+      if (last) {
+        double xt[NX];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) xt[i] = X[(size_t)N * NX + i] + slot[N * KD + i];
+        tsum += f.final_cost(xt);
+      }
+      tsum = wave_sum(tsum);
+      const bool traj_ok = __all(ok);
+      const double new_cost = traj_ok ? tsum : INFINITY;       // P:159-163, S:126-129
+      const double gain = (new_cost - cost) / pred;             // P:164-165
+      const bool success = (gain > 0.0) && bwd_ok;              // P:166 / S:137
+      const double shrink = fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0));
+      rp = success ? rp * shrink : rp * rinc;                   // P:167-171 / S:139-143
+      rinc = success ? 2.0 : 2.0 * rinc;                        // P:172 / S:144
+      bool take, end_iter, stop;
+      inner += 1;
+      if (mode == NOC_MODE_PAR) {
+        rp = fmin(fmax(rp, 1e-16), 1e16);                       // P:173
+        end_iter = success || inner > 500;                      // P:177-182
+        take = end_iter;                                        // last trial kept (P:175, P:184)
+        stop = end_iter && (hu < 1e-4 || it + 1 > 1000);        // P:199-202
+      } else {
+        take = success;                                         // S:145-146
+        end_iter = true;
+        stop = (hu < 1e-4) && bwd_ok;                           // S:157-161
+      }
+      if (take) {  // x <- x + dx, u <- u + du on the own chunk (its later readers are this lane)
+        for (int j = 0; j < len; ++j) {
+          const int k = start + j;
+          NOC_UNROLL for (int i = 0; i < NX; ++i) X[(size_t)k * NX + i] += slot[k * KD + i];
+          NOC_UNROLL for (int jj = 0; jj < NU; ++jj) U[(size_t)k * NU + jj] += slot[k * KD + NX + jj];
+        }
+        if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) X[(size_t)N * NX + i] += slot[N * KD + i];
+      }
+      __syncthreads();  // the next KKT solve overwrites the LDS slots read above
+      solves += 1;
+      it += end_iter ? 1 : 0;
+      if (stop) {                                               // barrier stage finished
+        total_it += it;                                         // P:239 / S:187
+        bp = bp / 5.0;                                          // P:238 / S:186
+        it = 0;
+        rp = 1.0;                                               // P:134 / S:110
+        rinc = 2.0;                                             // P:135 / S:111
+        stage_done = true;
+      } else if (mode == NOC_MODE_PAR) {
+        relinearize = end_iter;
+      } else {
+        relinearize = success;  // a rejected seq step only changes the regularisation
+      }
+      if (solves >= max_solves) {
+        capped = true;
+        break;
+      }
+    }
+    if (capped || !(bp > 1e-4)) break;                          // P:243-245
+  }
+  if (l == 0) {
+    w.bp[b] = bp;
+    w.rp[b] = rp;
+    w.rinc[b] = rinc;
+    w.cost[b] = cost;
+    w.hu[b] = hu;
+    w.gnorm[b] = gnorm;
+    w.it[b] = it;
+    w.inner[b] = inner;
+    w.total_it[b] = total_it;
+    w.kkt_solves[b] = solves;
+    w.kkt_active[b] = 0;
+    w.phase[b] = capped ? NOC_PHASE_SOLVE : NOC_PHASE_DONE;
+  }
+}
+
+template <int KIND, int NX, int NU>
+static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                          double bp0, int max_solves, hipStream_t s) {
+  size_t lds = kkt_lds_bytes_rt(NX, NU, w.N, PL);
+  if (lds == 0) return hipErrorInvalidValue;  // step does not fit in LDS: use the launch driver
+  lds += sizeof(IpmState) + 16;
+  hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU>), dim3(w.Bt), dim3(64), lds, s, p, w, mode,
+                     terminal, bp0, max_solves);
+  return hipGetLastError();
+}
+
+bool ipm_solve_supported(const noc_family& p, int N, int lanes) {
+  if (lanes != PL || !family_supported(p)) return false;
+  return kkt_lds_bytes_rt(p.nx, p.nu, N, PL) > 0;
+}
+
+hipError_t ipm_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal, double bp0,
+                     int max_solves, hipStream_t s) {
+  switch (p.kind) {
+    case NOC_FAMILY_PENDULUM:
+      if (p.nx == 2 && p.nu == 1) return solve_t<NOC_FAMILY_PENDULUM, 2, 1>(p, w, mode, terminal, bp0, max_solves, s);
+      break;
+    case NOC_FAMILY_CARTPOLE:
+      if (p.nx == 4 && p.nu == 1) return solve_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, w, mode, terminal, bp0, max_solves, s);
+      break;
+    case NOC_FAMILY_LINEAR:
+      if (p.nx == 2 && p.nu == 1) return solve_t<NOC_FAMILY_LINEAR, 2, 1>(p, w, mode, terminal, bp0, max_solves, s);
+      break;
+    default: break;
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace noc

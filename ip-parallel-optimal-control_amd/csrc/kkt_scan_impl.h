@@ -342,12 +342,12 @@ NOC_DEV double* lds_slots(int N) {
   return noc_smem + (size_t)(threadIdx.x / L) * per_traj;
 }
 
+// The whole KKT solve of trajectory `traj` by lane `l` of its L-lane segment (the kernel below;
+// also called by the persistent interior-point solver, ipm_persistent.hip).  With lds_out set and
+// dx = du = NULL the step stays in the LDS slots (x_s at slot s, u_s after it, x_N at slot N).
 template <int NX, int NU, int L, bool AFF, bool TILED>
-__global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
+NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
   constexpr int KD = kd_width<NX, NU>();
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int traj = tid / L;
-  const int l = tid % L;
   if (traj >= a.B) return;                     // uniform over the segment
   if (a.active && a.active[traj] == 0) return;  // uniform over the segment
   const int N = a.N;
@@ -678,6 +678,12 @@ __global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KK
       dst[i] = slot[s * KD + NX + (i - s * NU)];
     }
   }
+}
+
+template <int NX, int NU, int L, bool AFF, bool TILED>
+__global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  kkt_scan_wave<NX, NU, L, AFF, TILED>(a, tid / L, tid % L);
 }
 
 

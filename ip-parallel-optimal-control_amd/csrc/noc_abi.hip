@@ -274,6 +274,28 @@ int noc_ipm_step_main(const noc_family* fam, const noc_ipm_ws* ws, int mode, int
   return kkt_and_trial(fam, ws, mode, stream);
 }
 
+int noc_ipm_solve_supported(const noc_family* fam, int N, int lanes) {
+  return (fam && N >= 1 && noc::ipm_solve_supported(*fam, N, lanes)) ? 1 : 0;
+}
+
+int noc_ipm_solve(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, double bp0,
+                  int max_solves, void* stream) {
+  if (!fam) return fail(-2, "family is NULL");
+  int rc = check_ipm(fam, ws);
+  if (rc) return rc;
+  if (mode != NOC_MODE_PAR && mode != NOC_MODE_SEQ) return fail(-1, "bad mode");
+  if (terminal != NOC_TERMINAL_FINAL_COST && terminal != NOC_TERMINAL_STAGE0)
+    return fail(-1, "bad terminal option");
+  if (!(bp0 > 0.0)) return fail(-1, "bp0 must be > 0");
+  if (max_solves < 1) return fail(-1, "max_solves must be >= 1");
+  if (!noc::ipm_solve_supported(*fam, ws->N, ws->lanes))
+    return fail(-1, "persistent solve needs workspace lanes = 64 and a step that fits in LDS "
+                    "(noc_ipm_solve_supported)");
+  if (ws->Bt == 0) return 0;
+  return hip_status(noc::ipm_solve(*fam, *ws, mode, terminal, bp0, max_solves,
+                                   static_cast<hipStream_t>(stream)), "ipm_solve");
+}
+
 static int kkt_and_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* stream) {
   // the trial step needs dx, du only: gains stay on chip when they fit (ws->K, ws->d otherwise)
   const bool on_chip = noc_kkt_gains_on_chip(fam->nx, fam->nu, ws->N, ws->lanes) == 1;

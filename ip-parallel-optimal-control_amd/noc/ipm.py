@@ -18,9 +18,17 @@ import torch
 from . import _lib
 
 
+def persistent_supported(family, N: int) -> bool:
+    """noc_ipm_solve_supported: the whole-solve kernel handles this family / horizon (lanes 64)."""
+    lib = _lib.load()
+    return lib.noc_ipm_solve_supported(ctypes.byref(family.to_c()), int(N), 64) == 1
+
+
 class BatchedIPM:
     def __init__(self, family, N: int, batch: int, device="cuda", lanes: int = 0,
-                 overlap: Optional[bool] = None):
+                 overlap: Optional[bool] = None, persistent: bool = False):
+        """persistent=True: solve() runs the whole barrier schedule in one launch
+        (noc_ipm_solve, one wave per trajectory; forces lanes = 64)."""
         if not torch.cuda.is_available():
             raise _lib.NocError("no HIP device visible: the MI355X path has no CPU fallback")
         self.family = family
@@ -29,6 +37,12 @@ class BatchedIPM:
         self.nx, self.nu = family.nx, family.nu
         self.device = torch.device(device)
         lib = _lib.load()
+        self.persistent = bool(persistent)
+        if self.persistent:
+            if lanes not in (0, 64) or not persistent_supported(family, N):
+                raise _lib.NocError("persistent solve needs lanes = 64 and a supported family / "
+                                    "horizon (noc_ipm_solve_supported)")
+            lanes = 64
         self.lanes = lanes or lib.noc_kkt_default_lanes(family.nx, family.nu, N)
         if not lib.noc_family_supported(ctypes.byref(self.fam_c)):
             raise _lib.NocError(f"unsupported family kind={family.kind} nx={family.nx} nu={family.nu}")
@@ -111,10 +125,23 @@ class BatchedIPM:
     def all_done(self) -> bool:
         return self.active_count() == 0
 
+    def solve_persistent(self, mode: int = _lib.MODE_PAR,
+                         terminal: int = _lib.TERMINAL_FINAL_COST, bp0: float = 0.1,
+                         max_solves: int = 10 ** 7):
+        """The whole barrier schedule of every trajectory in ONE launch (noc_ipm_solve).
+        Returns the KKT solves of the slowest trajectory (the multi-launch loop's step count)."""
+        _lib.check(self._lib.noc_ipm_solve(ctypes.byref(self.fam_c), ctypes.byref(self.ws), mode,
+                                           terminal, float(bp0), int(max_solves), self._stream()),
+                   "noc_ipm_solve")
+        return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
+
     def solve(self, mode: int = _lib.MODE_PAR, terminal: int = _lib.TERMINAL_FINAL_COST,
               bp0: float = 0.1, poll_every: int = 8, max_steps: Optional[int] = None):
         """Run the barrier schedule to completion for every trajectory.  Returns the number of
         device iterations (= KKT solves of the slowest trajectory)."""
+        if self.persistent:
+            return self.solve_persistent(mode, terminal, bp0,
+                                         max_steps if max_steps is not None else 10 ** 7)
         self.init(bp0)
         steps = 0
         limit = max_steps if max_steps is not None else 10 ** 9

@@ -31,7 +31,10 @@ def _run(ocp: OCP, controls, initial_state, mode, terminal="final_cost", lanes=0
     if single:
         u, x0 = u[None], x0[None]
     Bt, N, _ = u.shape
-    eng = BatchedIPM(ocp.family, N, Bt, device=device, lanes=lanes)
+    from .ipm import persistent_supported
+    # whole solve in one launch when the family / horizon allows it (same results, lanes 64)
+    persistent = lanes in (0, 64) and persistent_supported(ocp.family, N)
+    eng = BatchedIPM(ocp.family, N, Bt, device=device, lanes=lanes, persistent=persistent)
     eng.load(u, x0)
     steps = eng.solve(mode=mode, terminal=_TERMINAL[terminal])
     U, iters, solves = eng.result()

@@ -153,3 +153,41 @@ def test_linear_demo_known_answer():
     r = np.zeros((N, 1))
     _, du, _ = O.dense_kkt(A, B, Q, R, M, r, np.diag(fam.wf), 0.0, x0)
     assert np.max(np.abs(U - du)) < 1e-8
+
+
+@pytest.mark.parametrize("name,N,Bt", [("pendulum", 60, 16), ("cartpole", 200, 64)])
+@pytest.mark.parametrize("mode", ["par", "seq"])
+def test_persistent_solve_equals_multilaunch_loop(name, N, Bt, mode):
+    """noc_ipm_solve (whole solve in one launch, one wave per trajectory) against the multi-launch
+    device loop at the same lanes (64): same arithmetic, so identical counters and iterates."""
+    from noc import problems, _lib
+    from noc.ipm import BatchedIPM
+    ocp = problems.make_problem(name, N)
+    x0, u0 = problems.initial_conditions(name, N, Bt, seed=21)
+    m = _lib.MODE_PAR if mode == "par" else _lib.MODE_SEQ
+    res = []
+    for persistent in (True, False):
+        eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=persistent)
+        eng.load(u0, x0)
+        eng.solve(mode=m)
+        torch.cuda.synchronize()
+        res.append([t.cpu().numpy() for t in eng.result()] + [eng.t["phase"].cpu().numpy()])
+    (Up, itp, sp, php), (Um, itm, sm, phm) = res
+    assert np.array_equal(itp, itm) and np.array_equal(sp, sm)
+    assert np.all(php == _lib.PHASE_DONE) and np.all(phm == _lib.PHASE_DONE)
+    assert np.max(np.abs(Up - Um)) <= 1e-12 * max(1.0, float(np.max(np.abs(Um))))
+
+
+def test_persistent_solve_respects_solve_cap():
+    """A trajectory that reaches max_solves stops (phase != DONE) -- every wave exits."""
+    from noc import problems, _lib
+    from noc.ipm import BatchedIPM
+    N, Bt = 50, 8
+    ocp = problems.pendulum(1.0 / N)
+    x0, u0 = problems.initial_conditions("pendulum", N, Bt, seed=4)
+    eng = BatchedIPM(ocp.family, N, Bt, persistent=True)
+    eng.load(u0, x0)
+    eng.solve_persistent(max_solves=5)
+    torch.cuda.synchronize()
+    assert np.all(eng.t["kkt_solves"].cpu().numpy() == 5)
+    assert np.all(eng.t["phase"].cpu().numpy() != _lib.PHASE_DONE)

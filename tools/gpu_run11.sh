@@ -1,0 +1,14 @@
+#!/bin/bash
+# Persistent whole-solve kernel: parity tests, then end-to-end timing vs the multi-launch loop.
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+cd "$R"; O=gpurun_out/r11; mkdir -p $O
+export TMPDIR=/tmp
+run() { local t=$1; local log=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$log" 2>&1; local rc=$?; echo "rc=$rc $log"; tail -4 "$O/$log"; if [ $rc -ne 0 ]; then exit $rc; fi; }
+run 300 pytest_ipm.log python -u -m pytest tests/test_ipm_gpu.py -x -v --timeout 120 --timeout-method thread
+run 200 ipm_c3_persist.log python tools/ipm_bench.py cartpole 200 4096 persistent
+run 200 ipm_c3_multi.log python tools/ipm_bench.py cartpole 200 4096 multi
+run 200 ipm_c2_persist.log python tools/ipm_bench.py pendulum 100 1024 persistent
+run 200 ipm_c2_multi.log python tools/ipm_bench.py pendulum 100 1024 multi
+run 200 ipm_c1_persist.log python tools/ipm_bench.py pendulum 50 1 persistent
+run 200 ipm_c1_multi.log python tools/ipm_bench.py pendulum 50 1 multi
+run 600 pytest_all.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread

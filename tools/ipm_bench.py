@@ -12,9 +12,10 @@ from noc.ipm import BatchedIPM
 name = sys.argv[1] if len(sys.argv) > 1 else "cartpole"
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 B = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
+persistent = (sys.argv[4] == "persistent") if len(sys.argv) > 4 else False
 ocp = problems.make_problem(name, N)
 x0, u0 = problems.initial_conditions(name, N, B, seed=11)
-eng = BatchedIPM(ocp.family, N, B)
+eng = BatchedIPM(ocp.family, N, B, persistent=persistent)
 eng.load(u0, x0)
 eng.solve(max_steps=16)   # warm-up (kernels loaded, caches)
 torch.cuda.synchronize()
@@ -24,7 +25,8 @@ steps = eng.solve()
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 U, its, solves = (t.cpu().numpy() for t in eng.result())
-print(json.dumps({"problem": name, "N": N, "B": B, "lanes": eng.lanes, "device_steps": steps,
+print(json.dumps({"problem": name, "N": N, "B": B, "lanes": eng.lanes, "persistent": persistent,
+                  "device_steps": steps,
                   "wall_s": dt, "ms_per_device_step": 1e3 * dt / steps,
                   "total_kkt_solves": int(solves.sum()), "kkt_solves_per_s": float(solves.sum() / dt),
                   "mean_outer_iters": float(its.mean()), "max_kkt_solves": int(solves.max()),

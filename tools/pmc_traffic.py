@@ -1,14 +1,15 @@
 #!/usr/bin/env python3
 """Per-launch HBM traffic of the KKT scan from rocprofv3 --pmc CSVs (separate FETCH_SIZE and
-WRITE_SIZE passes), corrected as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE (KB) counts half
+WRITE_SIZE passes) of the KKT kernel (name filter, default "kkt_"), corrected as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE (KB) counts half
 the bytes of 16-byte-per-lane coalesced reads on gfx950 (the tiled KKT loads are exactly that), so
 bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  Writes profiles/pmc_traffic.json."""
 import csv, json, sys
 fetch_csv, write_csv, key, out = sys.argv[1:5]
+kname = sys.argv[5] if len(sys.argv) > 5 else "kkt_"
 
 def mean(path, counter):
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if "kkt_scan" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+            if kname in r["Kernel_Name"] and r["Counter_Name"] == counter]
     return sum(vals) / len(vals), len(vals)
 
 f, nf = mean(fetch_csv, "FETCH_SIZE")
@@ -19,6 +20,7 @@ except Exception:
     d = {}
 d[key] = (2 * f + w) * 1024
 d[key + "_raw"] = {"FETCH_SIZE_KB": f, "WRITE_SIZE_KB": w, "launches": [nf, nw],
+                   "kernel_filter": kname,
                    "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 16B/lane reads)"}
 json.dump(d, open(out, "w"), indent=1)
 print(key, d[key])
