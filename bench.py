@@ -86,6 +86,37 @@ def residual_vs_seq_ref(out, ref, sample):
     return res
 
 
+def ipm_solve_rate(problem, N, B, rank):
+    """End-to-end: the whole interior-point solve (P:228-254) of the same B trajectories with the
+    persistent kernel (noc_ipm_solve, one launch), timed with HIP events.  Reported beside the KKT
+    metric: trajectories x Newton KKT solves actually performed / wall time."""
+    import torch
+    from noc import problems
+    from noc.ipm import BatchedIPM, persistent_supported
+    ocp = problems.make_problem(problem, N)
+    if not persistent_supported(ocp.family, N):
+        return {"skipped": "persistent solve unsupported for this family / horizon"}
+    x0, u0 = problems.initial_conditions(problem, N, B, seed=11 + rank)
+    eng = BatchedIPM(ocp.family, N, B, persistent=True)
+    eng.load(u0, x0)
+    eng.solve(max_steps=8)  # warm-up
+    eng.load(u0, x0)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    eng.solve()
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1)
+    U, its, solves = (t.cpu() for t in eng.result())
+    done = int((eng.t["phase"] == 3).sum().item())
+    return {"what": "whole barrier schedule, noc_ipm_solve (one wave per trajectory, one launch)",
+            "trajectories": B, "wall_ms": ms, "kkt_solves": int(solves.sum()),
+            "kkt_solves_per_s": float(solves.sum()) / (ms * 1e-3),
+            "mean_newton_iters": float(its.double().mean()), "max_kkt_solves": int(solves.max()),
+            "converged": done}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,6 +131,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-sample", type=int, default=512)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ipm", action="store_true", help="skip the end-to-end solve line")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -186,6 +218,8 @@ def main():
                      "algorithmic_bytes_per_launch": abytes, "kernel_ms": kern_ms},
         "feasible_fraction": feasible_frac,
     }
+    if not args.no_ipm:
+        result["ipm_solve"] = ipm_solve_rate(args.problem, N, B, rank)
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             sample = min(args.cpu_sample, B)
