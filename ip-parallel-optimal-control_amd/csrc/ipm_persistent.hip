@@ -349,12 +349,19 @@ __global__ __launch_bounds__(64, 2) void ipm_solve_kernel(noc_family prm, noc_ip
   }
 }
 
+// LDS of one persistent workgroup: the trajectory's KKT slots + the parked state.  Up to 64 KB
+// (long horizons at small batch, e.g. the reference's N = 1000 timing runs: 2 workgroups per CU).
+static size_t solve_lds_bytes(int nx, int nu, int N) {
+  const size_t slots = (size_t)(((long long)N * nu * (nx + 1) + nx + 1) & ~1LL) * sizeof(double);
+  const size_t bytes = slots + sizeof(IpmState) + 16;
+  return bytes <= 65536 ? bytes : 0;
+}
+
 template <int KIND, int NX, int NU>
 static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                           double bp0, int max_solves, hipStream_t s) {
-  size_t lds = kkt_lds_bytes_rt(NX, NU, w.N, PL);
+  const size_t lds = solve_lds_bytes(NX, NU, w.N);
   if (lds == 0) return hipErrorInvalidValue;  // step does not fit in LDS: use the launch driver
-  lds += sizeof(IpmState) + 16;
   hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU>), dim3(w.Bt), dim3(64), lds, s, p, w, mode,
                      terminal, bp0, max_solves);
   return hipGetLastError();
@@ -362,7 +369,8 @@ static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, in
 
 bool ipm_solve_supported(const noc_family& p, int N, int lanes) {
   if (lanes != PL || !family_supported(p)) return false;
-  return kkt_lds_bytes_rt(p.nx, p.nu, N, PL) > 0;
+  if (p.kind == NOC_FAMILY_LINEAR && p.nx == 8) return false;  // no nx=8 persistent instance
+  return solve_lds_bytes(p.nx, p.nu, N) > 0;
 }
 
 hipError_t ipm_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal, double bp0,

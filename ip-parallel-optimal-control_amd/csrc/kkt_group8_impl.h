@@ -1,0 +1,286 @@
+// nx = 8, nu = 4 horizon-sequential group KKT solve with LDS-DMA stage prefetch (fp64, gfx950).
+//
+// Same algorithm and lane mapping as kkt_group_kernel (kkt_group_impl.h: 8 trajectories per wave,
+// lane q of a group owns state column q), but the backward sweep is latency-hidden: while stage s
+// is computed from LDS buffer s&1, `global_load_lds_dwordx4` (no VGPR destination) streams stage
+// s-1's blocks of the wave's 8 trajectories into the other buffer (13.25 KB: A 4 KB, B 2 KB, Q 4 KB,
+// R 1 KB, M 2 KB, r 256 B).  Lanes then read operands from LDS.  The LDS image of A, B, Q, R is
+// row-rotated by the trajectory's slot g in the wave (row k of trajectory g stored at row slot
+// (k + g) mod rows), chosen on the SOURCE address of the DMA, so the column reads A[:, q] of the
+// 8 groups fall into different bank quarters (2-way instead of 8-way conflicts).
+// Contract of this path: Q and R are read through their upper triangle (lane q forms S_new[:, q]
+// from column q; the gathered S keeps entries i <= j), i.e. they are taken as symmetric.
+// The forward sweep keeps two stages of its row loads in flight in registers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "kkt_group_impl.h"
+
+#ifndef NOC_GROUP8_WAVES_PER_SIMD
+#define NOC_GROUP8_WAVES_PER_SIMD 2
+#endif
+
+namespace noc {
+
+namespace g8 {
+constexpr int NX = 8, NU = 4, TPW = 8;  // trajectories per wave
+// byte offsets of the fields inside one LDS stage buffer (8 trajectories each)
+constexpr int OA = 0, OB = 4096, OQ = 6144, OR = 10240, OM = 11264, ORV = 13312, OC = 13568,
+              OQV = 14080;
+constexpr int BUF_PLAIN = 13568;  // A..r
+constexpr int BUF_AFF = 14592;    // + c, q
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+// One DMA instruction's per-lane source offset (bytes, relative to field + traj0*N*sz, stage 0):
+// the row-rotated granule of trajectory t = traj0 + (wave-local slot).  sz: bytes per
+// trajectory-stage, rb: bytes per row, rows: rows per block (rotation modulus; 0 = none), i: the
+// instruction's index within the field.  Tail waves clamp t to the last trajectory (results of
+// clamped groups are never stored).
+NOC_DEV unsigned dma_off(int sz, int rb, int rows, int i, int lane, int traj0, int B, int N) {
+  const int gbyte = i * 1024 + lane * 16;  // byte offset inside the wave's field image
+  int t = gbyte / sz;
+  const int p = gbyte % sz;
+  const int slot = p / rb, off = p % rb;
+  const int row = rows ? ((slot - t) & (rows - 1)) : slot;
+  t = t < TPW ? t : TPW - 1;
+  t = (traj0 + t < B) ? t : B - 1 - traj0;
+  return (unsigned)((size_t)t * N * sz + row * rb + off);
+}
+
+NOC_DEV void glds16(const char* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)lds_dst, 16, 0, 0);
+}
+}  // namespace g8
+
+template <bool AFF>
+__global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kernel(KKTArgs a) {
+  using namespace g8;
+  constexpr int G = NX;
+  constexpr int BUF = AFF ? BUF_AFF : BUF_PLAIN;
+  extern __shared__ __attribute__((aligned(16))) double noc_smem[];
+  char* lds = reinterpret_cast<char*>(noc_smem);
+  const int lane = threadIdx.x;
+  const int g = lane / G;
+  const int q = lane % G;
+  const int uq = q % NU;
+  const int traj0 = blockIdx.x * TPW;
+  const int traj = traj0 + g;
+  const bool valid = traj < a.B && !(a.active && a.active[traj] == 0);
+  if (!__any(valid)) return;  // wave-uniform: nothing to do for this wave
+  const int N = a.N;
+  const size_t tN = (size_t)traj * N;
+  const int trajc = traj < a.B ? traj : a.B - 1;  // clamped index for loads of tail groups
+
+  if (a.mode != MODE_FWD) {
+    // per-lane DMA source offsets (A and Q share theirs; the stage step is uniform)
+    unsigned oA[4], oB[2], oM[2];
+    NOC_UNROLL for (int i = 0; i < 4; ++i) oA[i] = dma_off(512, 64, 8, i, lane, traj0, a.B, N);
+    NOC_UNROLL for (int i = 0; i < 2; ++i) {
+      oB[i] = dma_off(256, 32, 8, i, lane, traj0, a.B, N);
+      oM[i] = dma_off(256, 32, 0, i, lane, traj0, a.B, N);
+    }
+    const unsigned oR = dma_off(128, 32, 4, 0, lane, traj0, a.B, N);
+    const unsigned orv = dma_off(32, 32, 0, 0, lane < 16 ? lane : 0, traj0, a.B, N);
+    const unsigned ocq = dma_off(64, 64, 0, 0, lane < 32 ? lane : 0, traj0, a.B, N);
+    // wave-uniform bases of stage s of trajectory traj0
+    auto ubase = [&](const double* f, int sz, int s) {
+      return reinterpret_cast<const char*>(f) + ((size_t)traj0 * N + s) * sz;
+    };
+    auto issue = [&](int s, int buf) {
+      char* base = lds + buf * BUF;
+      const char* bA = ubase(a.A, 512, s);
+      const char* bQ = ubase(a.Q, 512, s);
+      const char* bB = ubase(a.Bm, 256, s);
+      const char* bM = ubase(a.M, 256, s);
+      NOC_UNROLL for (int i = 0; i < 4; ++i) {
+        glds16(bA + oA[i], base + OA + i * 1024);
+        glds16(bQ + oA[i], base + OQ + i * 1024);
+      }
+      NOC_UNROLL for (int i = 0; i < 2; ++i) {
+        glds16(bB + oB[i], base + OB + i * 1024);
+        glds16(bM + oM[i], base + OM + i * 1024);
+      }
+      glds16(ubase(a.R, 128, s) + oR, base + OR);
+      if (lane < 16) glds16(ubase(a.r, 32, s) + orv, base + ORV);
+      if constexpr (AFF) {
+        if (lane < 32) {
+          glds16(ubase(a.c ? a.c : a.A, 64, s) + ocq, base + OC);
+          glds16(ubase(a.q ? a.q : a.A, 64, s) + ocq, base + OQV);
+        }
+      }
+    };
+    const double reg = valid ? (a.reg ? a.reg[traj] : 0.0) : 0.0;
+    Sym<NX> S;
+    Vec<NX> v;
+    gload_sym<NX>(a.P + (size_t)trajc * NX * NX, S);
+    set_zero(v);
+    if constexpr (AFF) { if (a.p) gload<NX>(a.p + (size_t)trajc * NX, v.v); }
+    if (valid && a.S) {
+      const double* Pp = a.P + (size_t)traj * NX * NX;
+      double* dst = a.S + ((tN + traj + N) * NX + q) * NX;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) dst[i] = 0.5 * (Pp[q * NX + i] + Pp[i * NX + q]);
+    }
+    if (valid && a.v) a.v[(tN + traj + N) * NX + q] = (AFF && a.p) ? a.p[(size_t)traj * NX + q] : 0.0;
+    double pred = 0.0;
+    int feas = 1;
+    issue(N - 1, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int s = N - 1; s >= 0; --s) {
+      const int buf = (N - 1 - s) & 1;
+      if (s > 0) issue(s - 1, buf ^ 1);  // next stage streams in while this one is computed
+      const char* base = lds + buf * BUF;
+      // row-rotated LDS images of trajectory g (see header)
+      auto Arow = [&](int k) { return reinterpret_cast<const double*>(base + OA + g * 512 + ((k + g) & 7) * 64); };
+      auto Qrow = [&](int k) { return reinterpret_cast<const double*>(base + OQ + g * 512 + ((k + g) & 7) * 64); };
+      auto Brow = [&](int k) { return reinterpret_cast<const double*>(base + OB + g * 256 + ((k + g) & 7) * 32); };
+      auto Rrow = [&](int k) { return reinterpret_cast<const double*>(base + OR + g * 128 + ((k + g) & 3) * 32); };
+      const double* Mg = reinterpret_cast<const double*>(base + OM + g * 256);
+      const double* rg = reinterpret_cast<const double*>(base + ORV + g * 32);
+      double aq[NX], bq[NX], cc[NX];
+      NOC_UNROLL for (int k = 0; k < NX; ++k) {
+        aq[k] = Arow(k)[q];
+        bq[k] = Brow(k)[uq];
+        cc[k] = 0.0;
+      }
+      if constexpr (AFF) {
+        const double* cg = reinterpret_cast<const double*>(base + OC + g * 64);
+        if (a.c) NOC_UNROLL for (int k = 0; k < NX; ++k) cc[k] = cg[k];
+      }
+      double saq[NX], w[NX], gg[NX];
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        double t0 = 0.0, t1 = 0.0, t2 = v[i];
+        NOC_UNROLL for (int k = 0; k < NX; ++k) {
+          t0 += S(i, k) * aq[k];
+          t1 += S(i, k) * bq[k];
+          if constexpr (AFF) t2 += S(i, k) * cc[k];
+        }
+        saq[i] = t0;
+        w[i] = t1;
+        gg[i] = t2;
+      }
+      // Quu[:, uq] = R[:, uq] + reg e_uq + B' w ;  Qux[:, q] = M[q, :]' + B' SA_q ;  Qu = r + B' g
+      double quc[NU], qux[NU], qu[NU];
+      NOC_UNROLL for (int u = 0; u < NU; ++u) {
+        quc[u] = Rrow(u)[uq] + (u == uq ? reg : 0.0);
+        qux[u] = Mg[q * NU + u];
+        qu[u] = rg[u];
+      }
+      NOC_UNROLL for (int k = 0; k < NX; ++k) {
+        const double* br = Brow(k);
+        NOC_UNROLL for (int u = 0; u < NU; ++u) {
+          const double bku = br[u];
+          quc[u] += bku * w[k];
+          qux[u] += bku * saq[k];
+          qu[u] += bku * gg[k];
+        }
+      }
+      Sym<NU> Quu;
+      NOC_UNROLL for (int i = 0; i < NU; ++i)
+        NOC_UNROLL for (int j = i; j < NU; ++j) Quu(i, j) = gshfl(quc[i], j, G);
+      double Y[NU][2];
+      NOC_UNROLL for (int u = 0; u < NU; ++u) {
+        Y[u][0] = qux[u];
+        Y[u][1] = qu[u];
+      }
+      feas &= ldl_solve<NU, 2>(Quu, Y) ? 1 : 0;
+      double Kq[NU], dd[NU];
+      NOC_UNROLL for (int u = 0; u < NU; ++u) {
+        Kq[u] = -Y[u][0];
+        dd[u] = -Y[u][1];
+      }
+      const size_t si = tN + s;
+      if (valid) {
+        NOC_UNROLL for (int u = 0; u < NU; ++u) a.K[si * (NU * NX) + u * NX + q] = Kq[u];
+        if (q == 0) gstore<NU>(a.d + si * NU, dd);
+      }
+      NOC_UNROLL for (int i = 0; i < NU; ++i) {  // dV = d'Qu + 1/2 d'Quu d  (S:63)
+        double t = 0.0;
+        NOC_UNROLL for (int j = 0; j < NU; ++j) t += Quu(i, j) * dd[j];
+        pred += dd[i] * qu[i] + 0.5 * dd[i] * t;
+      }
+      // v_new[q] = q_q + A[:, q]' g + Qux[:, q]' d
+      double vq = 0.0;
+      if constexpr (AFF) {
+        if (a.q) vq = reinterpret_cast<const double*>(base + OQV + g * 64)[q];
+      }
+      NOC_UNROLL for (int k = 0; k < NX; ++k) vq += aq[k] * gg[k];
+      NOC_UNROLL for (int u = 0; u < NU; ++u) vq += qux[u] * dd[u];
+      // S_new[:, q] = Q[:, q] + A' SA_q + Qux' K[:, q]
+      double sn[NX];
+      NOC_UNROLL for (int i = 0; i < NX; ++i) sn[i] = Qrow(i)[q];
+      NOC_UNROLL for (int k = 0; k < NX; ++k) {
+        const double* ar = Arow(k);
+        NOC_UNROLL for (int i = 0; i < NX; ++i) sn[i] += ar[i] * saq[k];
+      }
+      NOC_UNROLL for (int u = 0; u < NU; ++u) {
+        NOC_UNROLL for (int i = 0; i < NX; ++i) sn[i] += gshfl(qux[u], i, G) * Kq[u];
+      }
+      NOC_UNROLL for (int i = 0; i < NX; ++i)
+        NOC_UNROLL for (int j = i; j < NX; ++j) S(i, j) = gshfl(sn[i], j, G);
+      NOC_UNROLL for (int i = 0; i < NX; ++i) v[i] = gshfl(vq, i, G);
+      if (valid && a.S) gstore<NX>(a.S + ((tN + traj + s) * NX + q) * NX, sn);
+      if (valid && a.v) a.v[(tN + traj + s) * NX + q] = vq;
+      // stage s-1 has landed in the other buffer (and this stage's reads of `buf` are done
+      // before the DMA after next overwrites it: the loads above were all consumed)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (valid && q == 0) {
+      if (a.pred) a.pred[traj] = pred;
+      if (a.feasible) a.feasible[traj] = feas;
+    }
+    if (a.mode == MODE_BWD) return;
+    __threadfence_block();  // this group's K, d stores are visible to its other lanes below
+  }
+
+  // ---------------- forward rollout of the closed loop (two stages of loads in flight) --------
+  const size_t tNc = (size_t)trajc * N;
+  Vec<NX> x;
+  set_zero(x);
+  if (a.x0) gload<NX>(a.x0 + (size_t)trajc * NX, x.v);
+  if (valid && a.dx) a.dx[(tN + traj) * NX + q] = a.x0 ? a.x0[(size_t)traj * NX + q] : 0.0;
+  auto load_f = [&](size_t si, double* kr, double* ar, double* br, double& dv, double& cv) {
+    gload<NX>(a.K + si * (NU * NX) + uq * NX, kr);
+    gload<NX>(a.A + si * (NX * NX) + q * NX, ar);
+    gload<NU>(a.Bm + si * (NX * NU) + q * NU, br);
+    dv = a.d[si * NU + uq];
+    cv = (AFF && a.c) ? a.c[si * NX + q] : 0.0;
+  };
+  double k0[NX], a0[NX], b0[NU], d0, c0, k1[NX], a1[NX], b1[NU], d1 = 0.0, c1 = 0.0;
+  load_f(tNc, k0, a0, b0, d0, c0);
+  if (N > 1) load_f(tNc + 1, k1, a1, b1, d1, c1);
+  for (int s = 0; s < N; ++s) {
+    double kr[NX], ar[NX], br[NU];
+    NOC_UNROLL for (int i = 0; i < NX; ++i) { kr[i] = k0[i]; ar[i] = a0[i]; k0[i] = k1[i]; a0[i] = a1[i]; }
+    NOC_UNROLL for (int i = 0; i < NU; ++i) { br[i] = b0[i]; b0[i] = b1[i]; }
+    const double dv = d0, cv = c0;
+    d0 = d1;
+    c0 = c1;
+    if (s + 2 < N) load_f(tNc + s + 2, k1, a1, b1, d1, c1);
+    double uu = dv;
+    NOC_UNROLL for (int k = 0; k < NX; ++k) uu += kr[k] * x[k];
+    double u[NU];
+    NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = gshfl(uu, j, G);
+    double xn = cv;
+    NOC_UNROLL for (int k = 0; k < NX; ++k) xn += ar[k] * x[k];
+    NOC_UNROLL for (int j = 0; j < NU; ++j) xn += br[j] * u[j];
+    const size_t si = tN + s;
+    if (valid && a.du && q < NU) a.du[si * NU + q] = uu;
+    if (valid && a.dx) a.dx[(tN + traj + s + 1) * NX + q] = xn;
+    NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = gshfl(xn, i, G);
+  }
+}
+
+static hipError_t launch_kkt_group8(const KKTArgs& a, hipStream_t stream) {
+  if (a.tiled) return hipErrorInvalidValue;   // natural layout only
+  if (!a.K || !a.d) return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((a.B + g8::TPW - 1) / g8::TPW);
+  const bool aff = a.q || a.c || a.p;
+  if (aff)
+    hipLaunchKernelGGL((kkt_group8_kernel<true>), dim3(grid), dim3(64), 2 * g8::BUF_AFF, stream, a);
+  else
+    hipLaunchKernelGGL((kkt_group8_kernel<false>), dim3(grid), dim3(64), 2 * g8::BUF_PLAIN, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace noc

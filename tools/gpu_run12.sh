@@ -1,0 +1,10 @@
+#!/bin/bash
+# LDS-DMA group8 kernel: parity, c4 timing; persistent solver with long horizons.
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+cd "$R"; O=gpurun_out/r12; mkdir -p $O
+export TMPDIR=/tmp
+run() { local t=$1; local log=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$log" 2>&1; local rc=$?; echo "rc=$rc $log"; tail -3 "$O/$log"; if [ $rc -ne 0 ]; then exit $rc; fi; }
+run 600 pytest_all.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+run 300 bench_c4.log python bench.py --problem linear8 --horizon 512 --batch 16384 --lanes 1 --steps 10 --warmup 2 --no-cpu
+run 200 ipm_pend1000.log python tools/ipm_bench.py pendulum 1000 1 persistent
+run 200 ipm_cart1000.log python tools/ipm_bench.py cartpole 1000 1 persistent
