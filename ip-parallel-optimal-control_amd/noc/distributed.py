@@ -30,11 +30,24 @@ def _comm_device():
         if dist.get_backend() == "nccl" else torch.device("cpu")
 
 
+def max_global(local: float) -> float:
+    """All-reduce(MAX) of one fp64 scalar (the convergence norm): one 8-byte collective."""
+    t = torch.tensor([float(local)], dtype=torch.float64, device=_comm_device())
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def any_active_global(local_active: int) -> bool:
     """All-reduce(MAX) of the local "still running" count: one 8-byte collective."""
     t = torch.tensor([int(local_active)], dtype=torch.int64, device=_comm_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return bool(t.item() > 0)
+
+
+def sum_global(local: int) -> int:
+    t = torch.tensor([int(local)], dtype=torch.int64, device=_comm_device())
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
 
 
 def gather_rows(local: np.ndarray, batch: int, world: int) -> np.ndarray:
@@ -55,10 +68,18 @@ def gather_rows(local: np.ndarray, batch: int, world: int) -> np.ndarray:
 
 def solve_sharded(ocp, controls, initial_state, mode=None, terminal=None,
                   engine_factory: Optional[Callable] = None, poll_every: int = 8,
-                  bp0: float = 0.1):
+                  bp0: float = 0.1, persistent: Optional[bool] = None,
+                  info: Optional[dict] = None):
     """Batched interior-point solve sharded over the process group.  Every rank passes the FULL
     batch (controls (B, N, nu), initial_state (B, nx)) and gets the full result back:
-    (controls*, iterations, kkt_solves)."""
+    (controls*, iterations, kkt_solves).
+
+    persistent (default: when the family / horizon supports it): every rank runs its shard's whole
+    solve in one launch (noc_ipm_solve) and the only collective on the solve path is the final
+    all-reduce(MAX) of the convergence norm max|Hu| (P:158) -- SURVEY.md §8e's "RCCL only for the
+    global convergence-norm all-reduce".  Otherwise the multi-launch loop polls the all-reduced
+    "still running" count every `poll_every` iterations.  `info` (a dict) receives
+    convergence_norm and not_done (global)."""
     from . import _lib
     mode = _lib.MODE_PAR if mode is None else mode
     terminal = _lib.TERMINAL_FINAL_COST if terminal is None else terminal
@@ -68,21 +89,36 @@ def solve_sharded(ocp, controls, initial_state, mode=None, terminal=None,
     B, N, _ = u.shape
     lo, hi = shard_bounds(B, world, rank)
     if engine_factory is None:
-        from .ipm import BatchedIPM
+        from .ipm import BatchedIPM, persistent_supported
+        if persistent is None:
+            persistent = persistent_supported(ocp.family, N)
 
         def engine_factory(n, b):
-            return BatchedIPM(ocp.family, n, b)
+            return BatchedIPM(ocp.family, n, b, persistent=bool(persistent))
     eng = engine_factory(N, max(hi - lo, 0))
-    if hi > lo:
-        eng.load(u[lo:hi], x0[lo:hi])
-        eng.init(bp0)
-    while True:
+    if persistent is None:
+        persistent = bool(getattr(eng, "persistent", False))
+    if persistent:
         if hi > lo:
-            for _ in range(poll_every):
-                eng.step(mode, terminal)
-        local = 0 if hi <= lo else eng.active_count()
-        if not any_active_global(local):
-            break
+            eng.load(u[lo:hi], x0[lo:hi])
+            eng.solve_persistent(mode, terminal, bp0)
+        norm = max_global(eng.convergence_norm() if hi > lo else 0.0)
+        not_done = sum_global(eng.active_count() if hi > lo else 0)
+    else:
+        if hi > lo:
+            eng.load(u[lo:hi], x0[lo:hi])
+            eng.init(bp0)
+        while True:
+            if hi > lo:
+                for _ in range(poll_every):
+                    eng.step(mode, terminal)
+            local = 0 if hi <= lo else eng.active_count()
+            if not any_active_global(local):
+                break
+        norm = max_global(eng.convergence_norm() if hi > lo else 0.0)
+        not_done = 0
+    if info is not None:
+        info.update(convergence_norm=norm, not_done=not_done)
     if hi > lo:
         U, it, solves = (t.cpu().numpy() for t in eng.result())
     else:

@@ -122,6 +122,10 @@ class BatchedIPM:
     def active_count(self) -> int:
         return int((self.t["phase"] != _lib.PHASE_DONE).sum().item())
 
+    def convergence_norm(self) -> float:
+        """max over this engine's trajectories of |Hu|_inf at their last linearisation (P:158)."""
+        return float(self.t["hu"].max().item()) if self.Bt else 0.0
+
     def all_done(self) -> bool:
         return self.active_count() == 0
 

@@ -293,3 +293,62 @@ def seq_bwd_pass(lqt: LQT):
 def seq_fwd_pass(lqt: LQT, x0, Kx, d):
     """paroc.seq_fwd_pass(lqt, x0, Kx, d) -> (u, x) (LM:75)."""
     return par_fwd_pass(lqt, x0, Kx, d)
+
+
+# ------------------------------------------------------------------------------------------------
+# closed-loop MPC (examples/linear_mpc_parallel.py:67-84)
+# ------------------------------------------------------------------------------------------------
+def mpc_loop(lqt: LQT, x0, steps: int, lanes: int = 0, graph: bool = True, chunk: int = 50):
+    """`par_mpc_loop` under `lax.scan` (LM:67-84): every MPC step solves the LQT from the current
+    state (par_bwd_pass + par_fwd_pass, here the fused KKT kernel with x0 = current state) and
+    applies the first control: u_t = u_par[0], x_{t+1} = x_par[1].
+
+    x0: (nx,) or (Bm, nx) -- a batch of independent MPC instances sharing the LQT.  Returns
+    (xs, us) of shapes (steps, [Bm,] nx) and (steps, [Bm,] nu), like the reference's scan outputs.
+    graph=True captures `chunk` consecutive steps in one HIP graph (torch.cuda.CUDAGraph) and
+    replays it, so a 5000-step loop costs 100 graph launches instead of 5000 x (solve + copies)."""
+    single = x0.dim() == 1
+    xcur = (x0.unsqueeze(0) if single else x0).to(torch.float64).contiguous().clone()
+    Bm, nx = xcur.shape
+    A, B, Q, R, M, r, q, c, P, p = lqt_to_canonical(lqt)
+    if lanes == 0 and A.shape[0] <= 32:
+        lanes = 1  # MPC horizons are short (LM: T = 5): the horizon-sequential group solve
+    exp = lambda t: None if t is None else t.unsqueeze(0).expand(Bm, *t.shape).contiguous()
+    A, B, Q, R, M, r, P = (exp(t) for t in (A, B, Q, R, M, r, P))
+    q, c, p = exp(_aff(q)), exp(_aff(c)), exp(_aff(p))
+    N, nu = A.shape[1], B.shape[-1]
+    out = kkt_solve(A, B, Q, R, M, r, P, x0=xcur, q=q, c=c, p=p, lanes=lanes, want_gains=False)
+    xs = torch.empty(steps, Bm, nx, dtype=torch.float64, device=xcur.device)
+    us = torch.empty(steps, Bm, nu, dtype=torch.float64, device=xcur.device)
+
+    def one_step(xs_t, us_t):
+        kkt_solve(A, B, Q, R, M, r, P, x0=xcur, q=q, c=c, p=p, lanes=lanes, out=out)
+        us_t.copy_(out.du[:, 0])
+        xs_t.copy_(out.dx[:, 1])
+        xcur.copy_(out.dx[:, 1])
+
+    t = 0
+    if graph and steps >= chunk:
+        stg_x = torch.empty(chunk, Bm, nx, dtype=torch.float64, device=xcur.device)
+        stg_u = torch.empty(chunk, Bm, nu, dtype=torch.float64, device=xcur.device)
+        side = torch.cuda.Stream(device=xcur.device)
+        side.wait_stream(torch.cuda.current_stream(xcur.device))
+        with torch.cuda.stream(side):  # warm-up on a side stream before capture (torch idiom)
+            one_step(stg_x[0], stg_u[0])
+        torch.cuda.current_stream(xcur.device).wait_stream(side)
+        xcur.copy_((x0.unsqueeze(0) if single else x0).to(torch.float64))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(chunk):
+                one_step(stg_x[i], stg_u[i])
+        while t + chunk <= steps:
+            g.replay()
+            xs[t:t + chunk].copy_(stg_x)
+            us[t:t + chunk].copy_(stg_u)
+            t += chunk
+    while t < steps:
+        one_step(xs[t], us[t])
+        t += 1
+    if single:
+        return xs[:, 0], us[:, 0]
+    return xs, us

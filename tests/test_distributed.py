@@ -38,6 +38,9 @@ class FakeEngine:
     def active_count(self):
         return int(np.sum(self.need > self.steps))
 
+    def convergence_norm(self):
+        return 1e-5 * float(np.max(self.x0[:, 0])) if len(self.x0) else 0.0
+
     def result(self):
         import torch
         done_at = np.minimum(self.need, self.steps)
@@ -45,7 +48,18 @@ class FakeEngine:
                 torch.as_tensor(done_at.astype(np.int32)), torch.as_tensor(self.need.astype(np.int32)))
 
 
-def _worker(rank, world, port, B, q):
+class FakePersistentEngine(FakeEngine):
+    """The whole solve in one call (noc_ipm_solve semantics): no polling."""
+    persistent = True
+
+    def solve_persistent(self, mode, terminal, bp0):
+        self.steps = int(self.need.max()) if len(self.need) else 0
+
+    def step(self, mode, terminal):  # must not be used on the persistent path
+        raise AssertionError("persistent engines are not stepped")
+
+
+def _worker(rank, world, port, B, q, persistent=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -55,14 +69,18 @@ def _worker(rank, world, port, B, q):
     u = np.arange(B * N, dtype=np.float64).reshape(B, N, nu)
     x0 = np.zeros((B, 2))
     x0[:, 0] = np.arange(B)
+    eng = FakePersistentEngine if persistent else FakeEngine
+    info = {}
     U, it, solves = D.solve_sharded(None, u, x0, mode=0, terminal=0,
-                                    engine_factory=lambda n, b: FakeEngine(n, b), poll_every=2)
-    q.put((rank, U, it, solves))
+                                    engine_factory=lambda n, b: eng(n, b), poll_every=2,
+                                    info=info)
+    q.put((rank, U, it, solves, info))
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("B", [7, 8, 1])
-def test_sharded_solve_world2_gloo(B):
+@pytest.mark.parametrize("persistent", [False, True])
+def test_sharded_solve_world2_gloo(B, persistent):
     from noc.distributed import shard_bounds
     world = 2
     spans = [shard_bounds(B, world, r) for r in range(world)]
@@ -71,7 +89,8 @@ def test_sharded_solve_world2_gloo(B):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, B, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, q, persistent))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -80,7 +99,10 @@ def test_sharded_solve_world2_gloo(B):
         assert p.exitcode == 0
     u = np.arange(B * 6, dtype=np.float64).reshape(B, 6, 1)
     need = (np.arange(B) % 5) + 3
-    for rank, U, it, solves in res:
+    for rank, U, it, solves, info in res:
         assert np.array_equal(U, u + np.arange(B)[:, None, None])   # order preserved
         assert np.array_equal(solves, need)
         assert np.array_equal(it, need)                            # every trajectory finished
+        # the global convergence norm is the all-reduce(MAX) over both ranks' shards
+        assert info["convergence_norm"] == pytest.approx(1e-5 * (B - 1))
+        assert info["not_done"] == 0

@@ -246,3 +246,44 @@ def test_group_solve_linear8_blocks_properties():
     assert relerr(du[sample].cpu(), ref["du"]) < RTOL
     assert relerr(res.pred[sample].cpu(), ref["pred"]) < RTOL
     assert bool(torch.all(res.feasible == 1))
+
+
+def _lm_lqt(T):
+    """examples/linear_mpc_parallel.py:24-64: RK4 double integrator (step 0.001), Q = P =
+    diag(1e2, 1), R = 0.1, tracking zero."""
+    from noc import problems
+    fam = problems.double_integrators(1, 0.001).family
+    A = np.repeat(np.asarray(fam.A, dtype=np.float64).reshape(1, 2, 2), T, 0)
+    B = np.repeat(np.asarray(fam.B, dtype=np.float64).reshape(1, 2, 1), T, 0)
+    Q = np.repeat(np.diag([1e2, 1.0])[None], T, 0)
+    R = np.repeat(0.1 * np.eye(1)[None], T, 0)
+    return A, B, Q, R
+
+
+@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("batched", [False, True])
+def test_mpc_loop_matches_oracle_closed_loop(graph, batched):
+    """LM:67-84 par_mpc_loop under lax.scan: each step solves the LQT from the current state and
+    applies u_par[0]; x_{t+1} = x_par[1].  Oracle: the sequential Riccati solve per step."""
+    from noc import lqt
+    from oracle import noc_oracle as O
+    T, steps = 5, 120
+    A, B, Q, R = _lm_lqt(T)
+    eye = lambda n: np.repeat(np.eye(n)[None], T, 0)
+    L = lqt.LQT(*(dev(t) for t in (A, B, np.zeros((T, 2)), np.diag([1e2, 1.0]), np.eye(2),
+                                    np.zeros(2), Q, eye(2), np.zeros((T, 2)), R, eye(1),
+                                    np.zeros((T, 1)), np.zeros((T, 2, 1)))))
+    x0s = np.array([[2.0, 1.0], [-1.0, 0.5], [0.3, -2.0]]) if batched else np.array([2.0, 1.0])
+    xs, us = lqt.mpc_loop(L, dev(x0s), steps, graph=graph, chunk=50)
+    torch.cuda.synchronize()
+    xs, us = xs.cpu().numpy(), us.cpu().numpy()
+    for b, x0 in enumerate(np.atleast_2d(x0s)):
+        x = x0.copy()
+        for t in range(steps):
+            dx, du = O.kkt_solve(A, B, Q, R, np.zeros((T, 2, 1)), np.zeros((T, 1)),
+                                 np.diag([1e2, 1.0]), 0.0, x0=x)[:2]
+            got_x = xs[t, b] if batched else xs[t]
+            got_u = us[t, b] if batched else us[t]
+            assert np.max(np.abs(got_u - du[0])) <= 1e-9 * max(1.0, np.abs(du[0]).max()), t
+            assert np.max(np.abs(got_x - dx[1])) <= 1e-10 * max(1.0, np.abs(dx[1]).max()), t
+            x = dx[1]
