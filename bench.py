@@ -146,14 +146,13 @@ def main():
     from noc import lqt, problems, _lib
 
     N, B = args.horizon, args.batch
-    if args.lanes == 1:  # horizon-sequential group solve: natural layout only
-        args.layout = "natural"
+    # lanes 8..64: the parallel-in-time scan on the lane-interleaved layout; lanes 1: the
+    # horizon-sequential group solve on the grouped layout (the nx = 8 default).  Either way the
+    # blocks are what the device linearisation writes for that solver.
     blocks = problems.make_bench_blocks(args.problem, N=N, batch=B, seed=1234 + rank,
-                                        lanes=args.lanes if args.lanes != 1 else 16,
-                                        natural=(args.layout == "natural"))
+                                        lanes=args.lanes, natural=(args.layout == "natural"))
     tb = blocks["tiled"]
-    nx, nu = tb.nx, tb.nu
-    lanes = args.lanes if args.lanes == 1 else tb.lanes
+    nx, nu, lanes = tb.nx, tb.nu, tb.lanes
     if args.layout == "tiled":
         out = lqt.kkt_solve_tiled(tb, reg=blocks["reg"], want_gains=False)
 

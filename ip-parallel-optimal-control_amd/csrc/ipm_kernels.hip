@@ -112,61 +112,65 @@ __global__ __launch_bounds__(64) void costate_scan_kernel(noc_family prm, noc_ip
   const double* xN = w.x + ((size_t)b * (N + 1) + N) * NX;
   double lamN[NX];
   NOC_UNROLL for (int i = 0; i < NX; ++i) lamN[i] = prm.wf[i] * f.err(xN, i);
-  // phase 1: chunk map lambda_start = G lambda_end + g
+  // phases 1-2 (L > 1): chunk maps and their scan; L = 1 (grouped layout, one lane per
+  // trajectory) sweeps the whole horizon from lambda_N directly
   Mat<NX, NX> G;
   Vec<NX> g;
-  set_identity(G);
   set_zero(g);
-  for (int k = start + len - 1; k >= start; --k) {
-    double A[NX * NX], cx[NX];
-    tload_rt<NX * NX>(w.A, L, ch.cmax, b, k - start, l, A);
-    tload_rt<NX>(w.cx, L, ch.cmax, b, k - start, l, cx);
-    Mat<NX, NX> Gn;
-    Vec<NX> gn;
-    NOC_UNROLL for (int i = 0; i < NX; ++i) {
-      double t = cx[i];
-      NOC_UNROLL for (int m = 0; m < NX; ++m) t += A[m * NX + i] * g[m];
-      gn[i] = t;
-      NOC_UNROLL for (int j = 0; j < NX; ++j) {
-        double u = 0.0;
-        NOC_UNROLL for (int m = 0; m < NX; ++m) u += A[m * NX + i] * G(m, j);
-        Gn(i, j) = u;
+  if constexpr (L > 1) {
+    // phase 1: chunk map lambda_start = G lambda_end + g
+    set_identity(G);
+    for (int k = start + len - 1; k >= start; --k) {
+      double A[NX * NX], cx[NX];
+      tload_rt<NX * NX>(w.A, L, ch.cmax, b, k - start, l, A);
+      tload_rt<NX>(w.cx, L, ch.cmax, b, k - start, l, cx);
+      Mat<NX, NX> Gn;
+      Vec<NX> gn;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        double t = cx[i];
+        NOC_UNROLL for (int m = 0; m < NX; ++m) t += A[m * NX + i] * g[m];
+        gn[i] = t;
+        NOC_UNROLL for (int j = 0; j < NX; ++j) {
+          double u = 0.0;
+          NOC_UNROLL for (int m = 0; m < NX; ++m) u += A[m * NX + i] * G(m, j);
+          Gn(i, j) = u;
+        }
       }
+      G = Gn;
+      g = gn;
     }
-    G = Gn;
-    g = gn;
-  }
-  if (last) {  // the last chunk ends at the terminal costate: its map becomes constant
-    NOC_UNROLL for (int i = 0; i < NX; ++i) {
-      double t = g[i];
-      NOC_UNROLL for (int m = 0; m < NX; ++m) t += G(i, m) * lamN[m];
-      g[i] = t;
-    }
-    set_zero(G);
-  }
-  // phase 2: reverse Hillis-Steele; lanes without a partner get their own (already constant) map
-#pragma unroll 1
-  for (int d = 1; d < L; d <<= 1) {
-    Mat<NX, NX> G2;
-    Vec<NX> g2;
-    shfl_down_arr<NX * NX>(G.v, G2.v, d, L);
-    shfl_down_arr<NX>(g.v, g2.v, d, L);
-    Mat<NX, NX> Gn;
-    NOC_UNROLL for (int i = 0; i < NX; ++i) {
-      double t = g[i];
-      NOC_UNROLL for (int m = 0; m < NX; ++m) t += G(i, m) * g2[m];
-      g[i] = t;
-      NOC_UNROLL for (int j = 0; j < NX; ++j) {
-        double u = 0.0;
-        NOC_UNROLL for (int m = 0; m < NX; ++m) u += G(i, m) * G2(m, j);
-        Gn(i, j) = u;
+    if (last) {  // the last chunk ends at the terminal costate: its map becomes constant
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        double t = g[i];
+        NOC_UNROLL for (int m = 0; m < NX; ++m) t += G(i, m) * lamN[m];
+        g[i] = t;
       }
+      set_zero(G);
     }
-    G = Gn;
+    // phase 2: reverse Hillis-Steele; lanes without a partner get their own (already constant) map
+  #pragma unroll 1
+    for (int d = 1; d < L; d <<= 1) {
+      Mat<NX, NX> G2;
+      Vec<NX> g2;
+      shfl_down_arr<NX * NX>(G.v, G2.v, d, L);
+      shfl_down_arr<NX>(g.v, g2.v, d, L);
+      Mat<NX, NX> Gn;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        double t = g[i];
+        NOC_UNROLL for (int m = 0; m < NX; ++m) t += G(i, m) * g2[m];
+        g[i] = t;
+        NOC_UNROLL for (int j = 0; j < NX; ++j) {
+          double u = 0.0;
+          NOC_UNROLL for (int m = 0; m < NX; ++m) u += G(i, m) * G2(m, j);
+          Gn(i, j) = u;
+        }
+      }
+      G = Gn;
+    }
   }
   // phase 3: sweep the chunk from its true end costate
   double lam[NX];
-  shfl_down_arr<NX>(g.v, lam, 1, L);
+  if constexpr (L > 1) shfl_down_arr<NX>(g.v, lam, 1, L);
   if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = lamN[i];
   double* LAM = w.lam + (size_t)b * (N + 1) * NX;
   if (last) gstore<NX>(LAM + (size_t)N * NX, lamN);
@@ -196,6 +200,9 @@ __global__ __launch_bounds__(64) void costate_scan_kernel(noc_family prm, noc_ip
     gstore<NX>(LAM + (size_t)k * NX, lam);
     cost += lc;
   }
+  // lambda at the chunk start := the scan's value g (not this lane's sweep): it is exactly the
+  // boundary costate the previous lane used, so every consumer of lambda_k sees one value
+  if (L > 1 && len > 0) gstore<NX>(LAM + (size_t)start * NX, g.v);
   NOC_UNROLL for (int off = L / 2; off > 0; off >>= 1) {
     cost += __shfl_xor(cost, off, L);
     g2s += __shfl_xor(g2s, off, L);
@@ -222,7 +229,8 @@ static void launch_costate(const noc_family& p, const noc_ipm_ws& w, int mode, h
     case 64: hipLaunchKernelGGL((costate_scan_kernel<KIND, NX, NU, 64>), dim3(grid), dim3(64), 0, s, p, w, mode); break;
     case 32: hipLaunchKernelGGL((costate_scan_kernel<KIND, NX, NU, 32>), dim3(grid), dim3(64), 0, s, p, w, mode); break;
     case 16: hipLaunchKernelGGL((costate_scan_kernel<KIND, NX, NU, 16>), dim3(grid), dim3(64), 0, s, p, w, mode); break;
-    default: hipLaunchKernelGGL((costate_scan_kernel<KIND, NX, NU, 8>), dim3(grid), dim3(64), 0, s, p, w, mode); break;
+    case 8: hipLaunchKernelGGL((costate_scan_kernel<KIND, NX, NU, 8>), dim3(grid), dim3(64), 0, s, p, w, mode); break;
+    default: hipLaunchKernelGGL((costate_scan_kernel<KIND, NX, NU, 1>), dim3(grid), dim3(64), 0, s, p, w, mode); break;
   }
 }
 

@@ -227,6 +227,9 @@ __global__ __launch_bounds__(64, 2) void ipm_solve_kernel(noc_family prm, noc_ip
           gstore<NX>(LAM + (size_t)k * NX, lam);
           csum += lc;
         }
+        // lambda at the chunk start := the scan's value g (not this lane's sweep): it is exactly the
+        // boundary costate the previous lane used, so every consumer of lambda_k sees one value
+        if (len > 0) gstore<NX>(LAM + (size_t)start * NX, g.v);
         NOC_UNROLL for (int off = PL / 2; off > 0; off >>= 1) {
           csum += __shfl_xor(csum, off, PL);
           g2s += __shfl_xor(g2s, off, PL);

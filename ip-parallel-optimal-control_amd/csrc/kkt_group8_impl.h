@@ -11,6 +11,10 @@
 // Contract of this path: Q and R are read through their upper triangle (lane q forms S_new[:, q]
 // from column q; the gathered S keeps entries i <= j), i.e. they are taken as symmetric.
 // The forward sweep keeps two stages of its row loads in flight in registers.
+// Two input layouts: natural (the ABI's [b][k][...]; each trajectory's 512/256/128 B blocks are
+// N*sz apart) and grouped (tiled with lanes = 1, small_linalg.h group_base: the wave's 8
+// trajectories of one stage contiguous per field, Q/R packed) -- what the IPM linearisation writes
+// for nx = 8.  Measured c4: grouped 5.69 ms, natural 6.24 ms.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -23,12 +27,18 @@
 namespace noc {
 
 namespace g8 {
-constexpr int NX = 8, NU = 4, TPW = 8;  // trajectories per wave
-// byte offsets of the fields inside one LDS stage buffer (8 trajectories each)
-constexpr int OA = 0, OB = 4096, OQ = 6144, OR = 10240, OM = 11264, ORV = 13312, OC = 13568,
-              OQV = 14080;
-constexpr int BUF_PLAIN = 13568;  // A..r
-constexpr int BUF_AFF = 14592;    // + c, q
+constexpr int NX = 8, NU = 4, TPW = 8;  // trajectories per wave (== GROUP_T)
+// Byte offsets of the fields inside one LDS stage buffer (8 trajectories each).  Natural layout:
+// Q, R as full matrices; grouped (tiled, lanes = 1) layout: Q, R packed symmetric.
+template <bool TILED>
+struct Lds {
+  static constexpr int QB = TILED ? 288 : 512;  // bytes of Q per trajectory
+  static constexpr int RB = TILED ? 80 : 128;   // bytes of R per trajectory
+  static constexpr int OA = 0, OB = 4096, OQ = 6144, OR = OQ + 8 * QB, OM = OR + 8 * RB,
+                       ORV = OM + 2048, OC = ORV + 256, OQV = OC + 512;
+  static constexpr int BUF_PLAIN = OC;        // A..r
+  static constexpr int BUF_AFF = OQV + 512;   // + c, q
+};
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
@@ -37,13 +47,16 @@ typedef __attribute__((address_space(1))) void glb_void;
 // trajectory-stage, rb: bytes per row, rows: rows per block (rotation modulus; 0 = none), i: the
 // instruction's index within the field.  Tail waves clamp t to the last trajectory (results of
 // clamped groups are never stored).
-NOC_DEV unsigned dma_off(int sz, int rb, int rows, int i, int lane, int traj0, int B, int N) {
+// grouped: the 8 trajectories' blocks are contiguous (stride sz; padding records cover the tail).
+NOC_DEV unsigned dma_off(int sz, int rb, int rows, int i, int lane, int traj0, int B, int N,
+                         bool grouped) {
   const int gbyte = i * 1024 + lane * 16;  // byte offset inside the wave's field image
   int t = gbyte / sz;
   const int p = gbyte % sz;
   const int slot = p / rb, off = p % rb;
   const int row = rows ? ((slot - t) & (rows - 1)) : slot;
   t = t < TPW ? t : TPW - 1;
+  if (grouped) return (unsigned)(t * sz + row * rb + off);
   t = (traj0 + t < B) ? t : B - 1 - traj0;
   return (unsigned)((size_t)t * N * sz + row * rb + off);
 }
@@ -53,11 +66,14 @@ NOC_DEV void glds16(const char* src, char* lds_dst) {
 }
 }  // namespace g8
 
-template <bool AFF>
+template <bool AFF, bool TILED>
 __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kernel(KKTArgs a) {
   using namespace g8;
+  using LD = Lds<TILED>;
   constexpr int G = NX;
-  constexpr int BUF = AFF ? BUF_AFF : BUF_PLAIN;
+  constexpr int BUF = AFF ? LD::BUF_AFF : LD::BUF_PLAIN;
+  constexpr int OA = LD::OA, OB = LD::OB, OQ = LD::OQ, OR = LD::OR, OM = LD::OM, ORV = LD::ORV,
+                OC = LD::OC, OQV = LD::OQV;
   extern __shared__ __attribute__((aligned(16))) double noc_smem[];
   char* lds = reinterpret_cast<char*>(noc_smem);
   const int lane = threadIdx.x;
@@ -74,34 +90,45 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
 
   if (a.mode != MODE_FWD) {
     // per-lane DMA source offsets (A and Q share theirs; the stage step is uniform)
-    unsigned oA[4], oB[2], oM[2];
-    NOC_UNROLL for (int i = 0; i < 4; ++i) oA[i] = dma_off(512, 64, 8, i, lane, traj0, a.B, N);
-    NOC_UNROLL for (int i = 0; i < 2; ++i) {
-      oB[i] = dma_off(256, 32, 8, i, lane, traj0, a.B, N);
-      oM[i] = dma_off(256, 32, 0, i, lane, traj0, a.B, N);
+    unsigned oA[4], oB[2], oM[2], oQ[4];
+    NOC_UNROLL for (int i = 0; i < 4; ++i) {
+      oA[i] = dma_off(512, 64, 8, i, lane, traj0, a.B, N, TILED);
+      // natural Q: full rows, rotated like A; grouped Q: packed (288 B), 3 instructions
+      oQ[i] = TILED ? dma_off(LD::QB, LD::QB, 0, i, lane, traj0, a.B, N, true) : oA[i];
     }
-    const unsigned oR = dma_off(128, 32, 4, 0, lane, traj0, a.B, N);
-    const unsigned orv = dma_off(32, 32, 0, 0, lane < 16 ? lane : 0, traj0, a.B, N);
-    const unsigned ocq = dma_off(64, 64, 0, 0, lane < 32 ? lane : 0, traj0, a.B, N);
-    // wave-uniform bases of stage s of trajectory traj0
+    NOC_UNROLL for (int i = 0; i < 2; ++i) {
+      oB[i] = dma_off(256, 32, 8, i, lane, traj0, a.B, N, TILED);
+      oM[i] = dma_off(256, 32, 0, i, lane, traj0, a.B, N, TILED);
+    }
+    const unsigned oR = TILED ? dma_off(LD::RB, LD::RB, 0, 0, lane < 40 ? lane : 0, traj0, a.B, N, true)
+                              : dma_off(128, 32, 4, 0, lane, traj0, a.B, N, false);
+    const unsigned orv = dma_off(32, 32, 0, 0, lane < 16 ? lane : 0, traj0, a.B, N, TILED);
+    const unsigned ocq = dma_off(64, 64, 0, 0, lane < 32 ? lane : 0, traj0, a.B, N, TILED);
+    // wave-uniform bases of stage s: trajectory traj0 (natural) or the wave's record (grouped)
     auto ubase = [&](const double* f, int sz, int s) {
-      return reinterpret_cast<const char*>(f) + ((size_t)traj0 * N + s) * sz;
+      const size_t rec = TILED ? ((size_t)(traj0 / TPW) * N + s) * TPW * sz
+                               : ((size_t)traj0 * N + s) * sz;
+      return reinterpret_cast<const char*>(f) + rec;
     };
     auto issue = [&](int s, int buf) {
       char* base = lds + buf * BUF;
       const char* bA = ubase(a.A, 512, s);
-      const char* bQ = ubase(a.Q, 512, s);
+      const char* bQ = ubase(a.Q, LD::QB, s);
       const char* bB = ubase(a.Bm, 256, s);
       const char* bM = ubase(a.M, 256, s);
-      NOC_UNROLL for (int i = 0; i < 4; ++i) {
-        glds16(bA + oA[i], base + OA + i * 1024);
-        glds16(bQ + oA[i], base + OQ + i * 1024);
+      NOC_UNROLL for (int i = 0; i < 4; ++i) glds16(bA + oA[i], base + OA + i * 1024);
+      if constexpr (TILED) {
+        glds16(bQ + oQ[0], base + OQ);
+        glds16(bQ + oQ[1], base + OQ + 1024);
+        if (lane < 16) glds16(bQ + oQ[2], base + OQ + 2048);
+      } else {
+        NOC_UNROLL for (int i = 0; i < 4; ++i) glds16(bQ + oQ[i], base + OQ + i * 1024);
       }
       NOC_UNROLL for (int i = 0; i < 2; ++i) {
         glds16(bB + oB[i], base + OB + i * 1024);
         glds16(bM + oM[i], base + OM + i * 1024);
       }
-      glds16(ubase(a.R, 128, s) + oR, base + OR);
+      if (!TILED || lane < 40) glds16(ubase(a.R, LD::RB, s) + oR, base + OR);
       if (lane < 16) glds16(ubase(a.r, 32, s) + orv, base + ORV);
       if constexpr (AFF) {
         if (lane < 32) {
@@ -132,9 +159,16 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       const char* base = lds + buf * BUF;
       // row-rotated LDS images of trajectory g (see header)
       auto Arow = [&](int k) { return reinterpret_cast<const double*>(base + OA + g * 512 + ((k + g) & 7) * 64); };
-      auto Qrow = [&](int k) { return reinterpret_cast<const double*>(base + OQ + g * 512 + ((k + g) & 7) * 64); };
       auto Brow = [&](int k) { return reinterpret_cast<const double*>(base + OB + g * 256 + ((k + g) & 7) * 32); };
-      auto Rrow = [&](int k) { return reinterpret_cast<const double*>(base + OR + g * 128 + ((k + g) & 3) * 32); };
+      // Q[i][q] and R[u][uq] (natural: row-rotated full matrices; grouped: packed upper triangle)
+      auto Qiq = [&](int i) {
+        if constexpr (TILED) return reinterpret_cast<const double*>(base + OQ + g * LD::QB)[Sym<NX>::idx(i, q)];
+        else return reinterpret_cast<const double*>(base + OQ + g * 512 + ((i + g) & 7) * 64)[q];
+      };
+      auto Ruq = [&](int u) {
+        if constexpr (TILED) return reinterpret_cast<const double*>(base + OR + g * LD::RB)[Sym<NU>::idx(u, uq)];
+        else return reinterpret_cast<const double*>(base + OR + g * 128 + ((u + g) & 3) * 32)[uq];
+      };
       const double* Mg = reinterpret_cast<const double*>(base + OM + g * 256);
       const double* rg = reinterpret_cast<const double*>(base + ORV + g * 32);
       double aq[NX], bq[NX], cc[NX];
@@ -162,7 +196,7 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       // Quu[:, uq] = R[:, uq] + reg e_uq + B' w ;  Qux[:, q] = M[q, :]' + B' SA_q ;  Qu = r + B' g
       double quc[NU], qux[NU], qu[NU];
       NOC_UNROLL for (int u = 0; u < NU; ++u) {
-        quc[u] = Rrow(u)[uq] + (u == uq ? reg : 0.0);
+        quc[u] = Ruq(u) + (u == uq ? reg : 0.0);
         qux[u] = Mg[q * NU + u];
         qu[u] = rg[u];
       }
@@ -191,8 +225,10 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       }
       const size_t si = tN + s;
       if (valid) {
-        NOC_UNROLL for (int u = 0; u < NU; ++u) a.K[si * (NU * NX) + u * NX + q] = Kq[u];
-        if (q == 0) gstore<NU>(a.d + si * NU, dd);
+        const size_t kb = TILED ? group_base(NU * NX, N, traj, s) : si * (NU * NX);
+        const size_t db = TILED ? group_base(NU, N, traj, s) : si * NU;
+        NOC_UNROLL for (int u = 0; u < NU; ++u) a.K[kb + u * NX + q] = Kq[u];
+        if (q == 0) gstore<NU>(a.d + db, dd);
       }
       NOC_UNROLL for (int i = 0; i < NU; ++i) {  // dV = d'Qu + 1/2 d'Quu d  (S:63)
         double t = 0.0;
@@ -208,7 +244,7 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       NOC_UNROLL for (int u = 0; u < NU; ++u) vq += qux[u] * dd[u];
       // S_new[:, q] = Q[:, q] + A' SA_q + Qux' K[:, q]
       double sn[NX];
-      NOC_UNROLL for (int i = 0; i < NX; ++i) sn[i] = Qrow(i)[q];
+      NOC_UNROLL for (int i = 0; i < NX; ++i) sn[i] = Qiq(i);
       NOC_UNROLL for (int k = 0; k < NX; ++k) {
         const double* ar = Arow(k);
         NOC_UNROLL for (int i = 0; i < NX; ++i) sn[i] += ar[i] * saq[k];
@@ -239,16 +275,25 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
   set_zero(x);
   if (a.x0) gload<NX>(a.x0 + (size_t)trajc * NX, x.v);
   if (valid && a.dx) a.dx[(tN + traj) * NX + q] = a.x0 ? a.x0[(size_t)traj * NX + q] : 0.0;
-  auto load_f = [&](size_t si, double* kr, double* ar, double* br, double& dv, double& cv) {
-    gload<NX>(a.K + si * (NU * NX) + uq * NX, kr);
-    gload<NX>(a.A + si * (NX * NX) + q * NX, ar);
-    gload<NU>(a.Bm + si * (NX * NU) + q * NU, br);
-    dv = a.d[si * NU + uq];
-    cv = (AFF && a.c) ? a.c[si * NX + q] : 0.0;
+  auto load_f = [&](int s, double* kr, double* ar, double* br, double& dv, double& cv) {
+    if constexpr (TILED) {
+      gload<NX>(a.K + group_base(NU * NX, N, trajc, s) + uq * NX, kr);
+      gload<NX>(a.A + group_base(NX * NX, N, trajc, s) + q * NX, ar);
+      gload<NU>(a.Bm + group_base(NX * NU, N, trajc, s) + q * NU, br);
+      dv = a.d[group_base(NU, N, trajc, s) + uq];
+      cv = (AFF && a.c) ? a.c[group_base(NX, N, trajc, s) + q] : 0.0;
+    } else {
+      const size_t si = tNc + s;
+      gload<NX>(a.K + si * (NU * NX) + uq * NX, kr);
+      gload<NX>(a.A + si * (NX * NX) + q * NX, ar);
+      gload<NU>(a.Bm + si * (NX * NU) + q * NU, br);
+      dv = a.d[si * NU + uq];
+      cv = (AFF && a.c) ? a.c[si * NX + q] : 0.0;
+    }
   };
   double k0[NX], a0[NX], b0[NU], d0, c0, k1[NX], a1[NX], b1[NU], d1 = 0.0, c1 = 0.0;
-  load_f(tNc, k0, a0, b0, d0, c0);
-  if (N > 1) load_f(tNc + 1, k1, a1, b1, d1, c1);
+  load_f(0, k0, a0, b0, d0, c0);
+  if (N > 1) load_f(1, k1, a1, b1, d1, c1);
   for (int s = 0; s < N; ++s) {
     double kr[NX], ar[NX], br[NU];
     NOC_UNROLL for (int i = 0; i < NX; ++i) { kr[i] = k0[i]; ar[i] = a0[i]; k0[i] = k1[i]; a0[i] = a1[i]; }
@@ -256,7 +301,7 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
     const double dv = d0, cv = c0;
     d0 = d1;
     c0 = c1;
-    if (s + 2 < N) load_f(tNc + s + 2, k1, a1, b1, d1, c1);
+    if (s + 2 < N) load_f(s + 2, k1, a1, b1, d1, c1);
     double uu = dv;
     NOC_UNROLL for (int k = 0; k < NX; ++k) uu += kr[k] * x[k];
     double u[NU];
@@ -272,14 +317,22 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
 }
 
 static hipError_t launch_kkt_group8(const KKTArgs& a, hipStream_t stream) {
-  if (a.tiled) return hipErrorInvalidValue;   // natural layout only
   if (!a.K || !a.d) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.B + g8::TPW - 1) / g8::TPW);
   const bool aff = a.q || a.c || a.p;
-  if (aff)
-    hipLaunchKernelGGL((kkt_group8_kernel<true>), dim3(grid), dim3(64), 2 * g8::BUF_AFF, stream, a);
-  else
-    hipLaunchKernelGGL((kkt_group8_kernel<false>), dim3(grid), dim3(64), 2 * g8::BUF_PLAIN, stream, a);
+  using LN = g8::Lds<false>;
+  using LT = g8::Lds<true>;
+  if (a.tiled) {
+    if (aff)
+      hipLaunchKernelGGL((kkt_group8_kernel<true, true>), dim3(grid), dim3(64), 2 * LT::BUF_AFF, stream, a);
+    else
+      hipLaunchKernelGGL((kkt_group8_kernel<false, true>), dim3(grid), dim3(64), 2 * LT::BUF_PLAIN, stream, a);
+  } else {
+    if (aff)
+      hipLaunchKernelGGL((kkt_group8_kernel<true, false>), dim3(grid), dim3(64), 2 * LN::BUF_AFF, stream, a);
+    else
+      hipLaunchKernelGGL((kkt_group8_kernel<false, false>), dim3(grid), dim3(64), 2 * LN::BUF_PLAIN, stream, a);
+  }
   return hipGetLastError();
 }
 

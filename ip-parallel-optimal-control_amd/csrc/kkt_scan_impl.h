@@ -342,11 +342,26 @@ NOC_DEV double* lds_slots(int N) {
   return noc_smem + (size_t)(threadIdx.x / L) * per_traj;
 }
 
+// Where the scan gets a stage's LQ blocks: from the KKTArgs arrays (tiled or natural layout).
+// The persistent solver passes a source that recomputes them from (x, u, lambda) instead.
+template <int NX, int NU, int L, bool AFF, bool TILED>
+struct ArgsSrc {
+  const KKTArgs& a;
+  int traj, l, cmax;
+  size_t tN;
+  NOC_DEV void stage(int s, int j, double reg, StageData<NX, NU>& st) const {
+    load_stage<NX, NU, L, AFF, TILED>(a, traj, tN + s, j, l, cmax, reg, st);
+  }
+  NOC_DEV void ab(int s, int j, Mat<NX, NX>& A, Mat<NX, NU>& Bm, Vec<NX>& c) const {
+    load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + s, j, l, cmax, A, Bm, c);
+  }
+};
+
 // The whole KKT solve of trajectory `traj` by lane `l` of its L-lane segment (the kernel below;
 // also called by the persistent interior-point solver, ipm_persistent.hip).  With lds_out set and
 // dx = du = NULL the step stays in the LDS slots (x_s at slot s, u_s after it, x_N at slot N).
-template <int NX, int NU, int L, bool AFF, bool TILED>
-NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
+template <int NX, int NU, int L, bool AFF, bool TILED, class SRC>
+NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, const SRC& src) {
   constexpr int KD = kd_width<NX, NU>();
   if (traj >= a.B) return;                     // uniform over the segment
   if (a.active && a.active[traj] == 0) return;  // uniform over the segment
@@ -379,7 +394,7 @@ NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
     }
     for (int s = start + len - 1; s >= start; --s) {
       StageData<NX, NU> st;
-      load_stage<NX, NU, L, AFF, TILED>(a, traj, tN + s, s - start, l, cmax, reg, st);
+      src.stage(s, s - start, reg, st);
       prepend<NX, NU, AFF>(e, st);
     }
     // ---------------- phase 2: reverse Hillis-Steele across lanes ----------------
@@ -411,7 +426,7 @@ NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
     double* skd = lds_slots<NX, NU, L>(N);  // K, d stay on chip for phase 4 when staged
     for (int s = start + len - 1; s >= start; --s) {
       StageData<NX, NU> st;
-      load_stage<NX, NU, L, AFF, TILED>(a, traj, tN + s, s - start, l, cmax, reg, st);
+      src.stage(s, s - start, reg, st);
       Mat<NX, NX> SA;
       Mat<NX, NU> SB;
       NOC_UNROLL for (int i = 0; i < NX; ++i) {
@@ -536,7 +551,7 @@ NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
       Mat<NX, NU> Bm;
       double Kk[NU * (NX + 1)];
       Vec<NX> cc;
-      load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + s, s - start, l, cmax, A, Bm, cc);
+      src.ab(s, s - start, A, Bm, cc);
       load_Kd<NX, NU, L, TILED>(a, traj, tN + s, s - start, l, cmax, Kk);
       Mat<NX, NX> F;
       Vec<NX> f;
@@ -612,7 +627,7 @@ NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
   double nK[NU * (NX + 1)];
   Vec<NX> nc;
   auto fetch = [&](int s) {
-    load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + s, s - start, l, cmax, nA, nB, nc);
+    src.ab(s, s - start, nA, nB, nc);
     if (kd_lds) {
       NOC_UNROLL for (int i = 0; i < NU * (NX + 1); ++i) nK[i] = slot[s * KD + i];
     } else {
@@ -678,6 +693,13 @@ NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
       dst[i] = slot[s * KD + NX + (i - s * NU)];
     }
   }
+}
+
+template <int NX, int NU, int L, bool AFF, bool TILED>
+NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
+  const int cmax = a.N / L + (a.N % L ? 1 : 0);
+  const ArgsSrc<NX, NU, L, AFF, TILED> src{a, traj, l, cmax, (size_t)traj * a.N};
+  kkt_scan_wave_src<NX, NU, L, AFF, TILED>(a, traj, l, src);
 }
 
 template <int NX, int NU, int L, bool AFF, bool TILED>

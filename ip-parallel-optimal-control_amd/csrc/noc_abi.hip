@@ -7,6 +7,7 @@
 
 #include "../../include/noc_hip.h"
 #include "noc_internal.h"
+#include "small_linalg.h"
 
 namespace {
 thread_local std::string g_last_error;
@@ -60,7 +61,9 @@ hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t
 // horizons need the lanes for parallelism (L = 64 at c2, N = 100).
 int kkt_default_lanes(int nx, int nu, int N) {
   (void)nu;
-  if (nx >= 8) return 16;
+  // nx = 8: the horizon-sequential group solve (lanes 1) -- c4: 6.1 ms vs 47-55 ms for the scan,
+  // whose nx = 8 element spills (profiles/r01/session2/r9_sweep_c4.log, bench_c4_dma.log)
+  if (nx >= 8) return 1;
   return N >= 160 ? 32 : 64;
 }
 }  // namespace noc
@@ -118,7 +121,8 @@ static int kkt_common(int mode, int tiled, int nx, int nu, int N, int B, int lan
   a.ablate = g_ablate;
   a.tiled = tiled;
   if (tiled && lanes == 0) return fail(-1, "the tiled layout needs an explicit lanes value");
-  if (tiled && lanes == 1) return fail(-1, "lanes = 1 (group solve) reads the natural layout");
+  if (tiled && lanes == 1 && !(nx == 8 && nu == 4))
+    return fail(-1, "the grouped (lanes = 1) tiled layout is supported for (nx, nu) = (8, 4)");
   (void)bwd;
   (void)fwd;
   const int L = lanes ? lanes : noc::kkt_default_lanes(nx, nu, N);
@@ -151,6 +155,8 @@ int noc_kkt_solve_tiled(int nx, int nu, int N, int B, int lanes, const double* A
 
 long long noc_tiled_doubles(int N, int B, int lanes, int E) {
   if (N < 1 || B < 0 || lanes < 1 || E < 1) return -1;
+  if (lanes == 1)  // grouped layout: whole records of GROUP_T trajectories
+    return (long long)((B + noc::GROUP_T - 1) / noc::GROUP_T) * noc::GROUP_T * N * E;
   const long long cmax = (N + lanes - 1) / lanes;
   return (long long)B * cmax * E * lanes;
 }
@@ -159,7 +165,8 @@ int noc_relayout(int direction, int E, int sym_n, int N, int B, int lanes, const
                  double* dst, void* stream) {
   if (direction != 0 && direction != 1) return fail(-1, "direction must be 0 or 1");
   if (N < 1 || B < 0 || E < 1) return fail(-1, "bad dims");
-  if (lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64) return fail(-1, "lanes must be 8/16/32/64");
+  if (lanes != 1 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64)
+    return fail(-1, "lanes must be 1/8/16/32/64");
   if (sym_n > 0 && E != sym_n * (sym_n + 1) / 2) return fail(-1, "E must be sym_n(sym_n+1)/2");
   if (!src || !dst) return fail(-2, "NULL pointer");
   return hip_status(noc::relayout(direction, E, sym_n, N, B, lanes, src, dst,
@@ -191,8 +198,10 @@ int noc_family_supported(const noc_family* fam) {
 static int check_ipm(const noc_family* fam, const noc_ipm_ws* ws) {
   if (!ws) return fail(-2, "workspace is NULL");
   if (ws->Bt < 0 || ws->N < 1) return fail(-1, "workspace dims: need Bt >= 0, N >= 1");
-  if (ws->lanes != 8 && ws->lanes != 16 && ws->lanes != 32 && ws->lanes != 64)
-    return fail(-1, "workspace lanes must be 8, 16, 32 or 64");
+  if (ws->lanes != 1 && ws->lanes != 8 && ws->lanes != 16 && ws->lanes != 32 && ws->lanes != 64)
+    return fail(-1, "workspace lanes must be 1, 8, 16, 32 or 64");
+  if (ws->lanes == 1 && fam && !(fam->nx == 8 && fam->nu == 4))
+    return fail(-1, "workspace lanes = 1 (grouped layout) is supported for nx = 8, nu = 4");
   if (fam && !noc::family_supported(*fam))
     return fail(-1, "unsupported problem family (kind/nx/nu)");
   const void* req[] = {ws->x, ws->u, ws->x0, ws->A, ws->B, ws->Q, ws->R, ws->M, ws->r, ws->P,

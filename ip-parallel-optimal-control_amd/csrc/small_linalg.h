@@ -96,9 +96,17 @@ NOC_DEV void gstore_sym(double* __restrict__ dst, const Sym<N>& S) {
 //   E even: (((traj*cmax + j)*(E/2) + e/2)*L + l)*2 + (e&1)     (16-byte granules)
 //   E odd : ((traj*cmax + j)*E + e)*L + l                         (8-byte granules)
 // so one wave-wide load of a granule is L*16 (L*8) contiguous bytes.
+// lanes = 1 ("grouped" layout of the horizon-sequential group solve): records of GROUP_T
+// trajectories, [traj / GROUP_T][stage][traj % GROUP_T][e] -- one wave's 8 trajectories of one
+// stage are GROUP_T * E contiguous doubles per field (cmax == N when L == 1).
+constexpr int GROUP_T = 8;
+NOC_DEV size_t group_base(int E, int N, int traj, int s) {
+  return (((size_t)(traj / GROUP_T) * N + s) * GROUP_T + (traj % GROUP_T)) * E;
+}
 template <int E, int L>
 NOC_DEV size_t tile_base(int traj, int j, int l, int cmax) {
-  if constexpr (E % 2 == 0) return (((size_t)traj * cmax + j) * (E / 2) * L + l) * 2;
+  if constexpr (L == 1) return group_base(E, cmax, traj, j);
+  else if constexpr (E % 2 == 0) return (((size_t)traj * cmax + j) * (E / 2) * L + l) * 2;
   else return ((size_t)traj * cmax + j) * E * L + l;
 }
 template <int E, int L>
@@ -126,6 +134,7 @@ NOC_DEV void tstore(double* __restrict__ base, int traj, int j, int l, int cmax,
 }
 // runtime-E variant (relayout / linearisation kernels)
 NOC_DEV size_t tile_index(int E, int L, int cmax, int traj, int j, int l, int e) {
+  if (L == 1) return group_base(E, cmax, traj, j) + e;
   if ((E & 1) == 0) return (((size_t)traj * cmax + j) * (E / 2) + (e >> 1)) * (2 * L) + 2 * l + (e & 1);
   return (((size_t)traj * cmax + j) * E + e) * L + l;
 }

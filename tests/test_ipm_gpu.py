@@ -191,3 +191,30 @@ def test_persistent_solve_respects_solve_cap():
     torch.cuda.synchronize()
     assert np.all(eng.t["kkt_solves"].cpu().numpy() == 5)
     assert np.all(eng.t["phase"].cpu().numpy() != _lib.PHASE_DONE)
+
+
+def test_linear8_ipm_uses_group_solve_and_is_exact():
+    """Four stacked double integrators (nx=8, nu=4; the c4 family): the IPM workspace defaults to
+    the grouped layout + horizon-sequential group solve (lanes 1); the unconstrained LQ problem is
+    solved exactly by one Newton step -- compare with the dense KKT solution per trajectory."""
+    from noc import problems
+    from noc.ipm import BatchedIPM
+    from oracle import noc_oracle as O
+    N, Bt = 24, 11   # a partial last record of the grouped layout
+    ocp = problems.double_integrators(4, 0.01)
+    fam = ocp.family
+    x0, u0 = problems.initial_conditions("linear8", N, Bt, seed=5)
+    eng = BatchedIPM(fam, N, Bt)
+    assert eng.lanes == 1
+    eng.load(u0, x0)
+    eng.solve()
+    torch.cuda.synchronize()
+    U = eng.result()[0].cpu().numpy()
+    A = np.repeat(np.asarray(fam.A, np.float64).reshape(1, 8, 8), N, 0)
+    B = np.repeat(np.asarray(fam.B, np.float64).reshape(1, 8, 4), N, 0)
+    Q = np.repeat(np.diag(fam.wx)[None], N, 0)
+    R = np.repeat(np.diag(fam.wu)[None], N, 0)
+    for b in range(Bt):
+        _, du, _ = O.dense_kkt(A, B, Q, R, np.zeros((N, 8, 4)), np.zeros((N, 4)),
+                               np.diag(fam.wf), 0.0, x0[b])
+        assert np.max(np.abs(U[b] - du)) < 1e-8 * max(1.0, np.abs(du).max())

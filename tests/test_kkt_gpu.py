@@ -141,11 +141,12 @@ def test_lqt_tracking_form_adapter():
     assert bool(feas)
 
 
-@pytest.mark.parametrize("nx,nu", [(2, 1), (4, 1), (8, 4)])
-@pytest.mark.parametrize("lanes", [64, 32, 16, 8])
+@pytest.mark.parametrize("nx,nu,lanes", [(nx, nu, L) for nx, nu in [(2, 1), (4, 1), (8, 4)]
+                                          for L in (64, 32, 16, 8)] + [(8, 4, 1)])
 @pytest.mark.parametrize("N", [1, 13, 200])
 def test_tiled_layout_kkt_matches_oracle(nx, nu, lanes, N):
-    """The tiled (lane-interleaved, Q/R packed) layout the IPM workspace uses."""
+    """The tiled layout the IPM workspace uses: lane-interleaved for the scan (lanes 8-64),
+    grouped records of 8 trajectories for the group solve (lanes 1); Q/R packed."""
     from noc import lqt
     case = rand_lq(77 * nx + N + lanes, 5, N, nx, nu)
     ref = oracle_batch(case)
@@ -161,7 +162,7 @@ def test_tiled_layout_kkt_matches_oracle(nx, nu, lanes, N):
     assert np.array_equal(out.feasible.cpu().numpy().astype(bool), ref["feasible"].astype(bool))
 
 
-@pytest.mark.parametrize("lanes", [64, 16])
+@pytest.mark.parametrize("lanes", [64, 16, 1])
 def test_tile_untile_roundtrip(lanes):
     from noc import lqt
     rng = np.random.default_rng(0)

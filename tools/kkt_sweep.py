@@ -29,11 +29,10 @@ def main():
         name, N, B = CONFIGS[cname]
         times, outs, tbs = {}, {}, {}
         for L in [int(x) for x in args.lanes.split(",")]:
-            # lanes = 1 (horizon-sequential group solve) reads the natural layout only
-            blk = problems.make_bench_blocks(name, N=N, batch=B, seed=7, lanes=L if L > 1 else 16)
+            blk = problems.make_bench_blocks(name, N=N, batch=B, seed=7, lanes=L)
             tb = blk["tiled"]
             nx, nu = tb.nx, tb.nu
-            for layout in (args.layouts.split(",") if L > 1 else ["natural"]):
+            for layout in args.layouts.split(","):
                 key = (L, layout)
                 times[key] = []
                 if layout == "tiled":
