@@ -293,16 +293,20 @@ __global__ __launch_bounds__(256) void trial_kernel(noc_family prm, noc_ipm_ws w
   const double* DX = w.dx + (size_t)b * (N + 1) * NX;
   const double* U = w.u + (size_t)b * N * NU;
   const double* DU = w.du + (size_t)b * N * NU;
+  // lane l sums the stages of horizon chunk l (the 64-lane chunk geometry) and the last lane adds
+  // the final cost: the same summation order as the persistent solver (ipm_persistent.hip), so
+  // both drivers take identical accept / reject decisions
   double csum = 0.0;
   int ok = 1;
-  for (int k = lane; k < N; k += 64) {
+  const Chunks ch(N, 64);
+  for (int k = ch.start(lane); k < ch.start(lane) + ch.len(lane); ++k) {
     double xt[NX], ut[NU];
     NOC_UNROLL for (int i = 0; i < NX; ++i) xt[i] = X[(size_t)k * NX + i] + DX[(size_t)k * NX + i];
     NOC_UNROLL for (int j = 0; j < NU; ++j) ut[j] = U[(size_t)k * NU + j] + DU[(size_t)k * NU + j];
     ok &= f.feasible(ut) ? 1 : 0;
     csum += f.stage_cost(xt, ut, bp);
   }
-  if (lane == 0) {
+  if (lane == 63) {
     double xt[NX];
     NOC_UNROLL for (int i = 0; i < NX; ++i) xt[i] = X[(size_t)N * NX + i] + DX[(size_t)N * NX + i];
     csum += f.final_cost(xt);

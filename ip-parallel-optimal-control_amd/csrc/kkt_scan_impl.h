@@ -27,6 +27,12 @@
 #include "small_linalg.h"
 #include "noc_internal.h"
 
+// The scan is compiled with cross-statement FMA contraction (the library default is
+// -ffp-contract=on, which keeps the interior-point drivers' arithmetic independent of inlining
+// context); every kernel that inlines this scan sees the same pragma, so the standalone and the
+// persistent KKT solves still round identically.
+#pragma clang fp contract(fast)
+
 #ifndef NOC_KKT_WAVES_PER_SIMD
 #define NOC_KKT_WAVES_PER_SIMD 2
 #endif
@@ -746,3 +752,5 @@ static hipError_t dispatch_aff(const KKTArgs& a, int lanes, hipStream_t stream) 
 }
 
 }  // namespace noc
+
+#pragma clang fp contract(on)

@@ -82,7 +82,9 @@ def solve_sharded(ocp, controls, initial_state, mode=None, terminal=None,
     convergence_norm and not_done (global)."""
     from . import _lib
     mode = _lib.MODE_PAR if mode is None else mode
-    terminal = _lib.TERMINAL_FINAL_COST if terminal is None else terminal
+    if terminal is None:
+        from .ipm import default_terminal
+        terminal = default_terminal(mode)
     world, rank = dist.get_world_size(), dist.get_rank()
     u = np.asarray(controls, dtype=np.float64)
     x0 = np.asarray(initial_state, dtype=np.float64)

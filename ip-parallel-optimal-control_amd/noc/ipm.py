@@ -18,6 +18,12 @@ import torch
 from . import _lib
 
 
+def default_terminal(mode: int) -> int:
+    """The terminal Hessian the reference uses in each mode: par_Newton's LQT has XT = Q[0]
+    (noc/par_interior_point_newton.py:73); the seq bwd_pass uses hessian(final_cost) (S:66)."""
+    return _lib.TERMINAL_STAGE0 if mode == _lib.MODE_PAR else _lib.TERMINAL_FINAL_COST
+
+
 def persistent_supported(family, N: int) -> bool:
     """noc_ipm_solve_supported: the whole-solve kernel handles this family / horizon (lanes 64)."""
     lib = _lib.load()
@@ -129,20 +135,23 @@ class BatchedIPM:
     def all_done(self) -> bool:
         return self.active_count() == 0
 
-    def solve_persistent(self, mode: int = _lib.MODE_PAR,
-                         terminal: int = _lib.TERMINAL_FINAL_COST, bp0: float = 0.1,
-                         max_solves: int = 10 ** 7):
+    def solve_persistent(self, mode: int = _lib.MODE_PAR, terminal: Optional[int] = None,
+                         bp0: float = 0.1, max_solves: int = 10 ** 7):
         """The whole barrier schedule of every trajectory in ONE launch (noc_ipm_solve).
-        Returns the KKT solves of the slowest trajectory (the multi-launch loop's step count)."""
+        Returns the KKT solves of the slowest trajectory (the multi-launch loop's step count).
+        terminal=None: the reference's choice for the mode (par: XT = Q[0], P:73; seq: S:66)."""
+        terminal = default_terminal(mode) if terminal is None else terminal
         _lib.check(self._lib.noc_ipm_solve(ctypes.byref(self.fam_c), ctypes.byref(self.ws), mode,
                                            terminal, float(bp0), int(max_solves), self._stream()),
                    "noc_ipm_solve")
         return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
 
-    def solve(self, mode: int = _lib.MODE_PAR, terminal: int = _lib.TERMINAL_FINAL_COST,
+    def solve(self, mode: int = _lib.MODE_PAR, terminal: Optional[int] = None,
               bp0: float = 0.1, poll_every: int = 8, max_steps: Optional[int] = None):
         """Run the barrier schedule to completion for every trajectory.  Returns the number of
-        device iterations (= KKT solves of the slowest trajectory)."""
+        device iterations (= KKT solves of the slowest trajectory).  terminal=None: the
+        reference's choice for the mode (par: XT = Q[0], P:73; seq: hessian(final_cost), S:66)."""
+        terminal = default_terminal(mode) if terminal is None else terminal
         if self.persistent:
             return self.solve_persistent(mode, terminal, bp0,
                                          max_steps if max_steps is not None else 10 ** 7)

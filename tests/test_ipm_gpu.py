@@ -61,7 +61,7 @@ def test_pendulum_par_solve_matches_oracle():
     x0 = np.array([0.1, -0.1])
     U, it, info = par_interior_point_optimal_control(ocp, u0, x0, return_info=True)
     prob = _oracle_problem("pendulum", N)
-    Ur, itr, solves_r = O.par_interior_point_optimal_control(prob, u0, x0)
+    Ur, itr, solves_r = O.par_interior_point_optimal_control(prob, u0, x0, terminal="stage0")
     assert it == itr == 70
     assert info["kkt_solves"] == solves_r == 87
     c = prob.total_cost(O.rollout(prob.dynamics, U, x0), U, 0.0)
@@ -96,7 +96,7 @@ def test_batched_solve_equals_individual_oracle_runs():
     U, its, info = par_interior_point_optimal_control(ocp, u0, x0, return_info=True)
     prob = _oracle_problem("pendulum", N)
     for b in range(Bt):
-        Ur, itr, sr = O.par_interior_point_optimal_control(prob, u0[b], x0[b])
+        Ur, itr, sr = O.par_interior_point_optimal_control(prob, u0[b], x0[b], terminal="stage0")
         assert its[b] == itr and info["kkt_solves"][b] == sr
         assert np.max(np.abs(U[b] - Ur)) < 1e-6
 
@@ -110,15 +110,16 @@ def test_cartpole_par_solve_matches_oracle():
     x0, u0 = problems.initial_conditions("cartpole", N, 1, seed=3)
     U, it, info = par_interior_point_optimal_control(ocp, u0[0], x0[0], return_info=True)
     prob = _oracle_problem("cartpole", N)
-    Ur, itr, sr = O.par_interior_point_optimal_control(prob, u0[0], x0[0])
+    Ur, itr, sr = O.par_interior_point_optimal_control(prob, u0[0], x0[0], terminal="stage0")
     assert it == itr and info["kkt_solves"] == sr
     c = prob.total_cost(O.rollout(prob.dynamics, U, x0[0]), U, 0.0)
     cr = prob.total_cost(O.rollout(prob.dynamics, Ur, x0[0]), Ur, 0.0)
     assert abs(c - cr) <= 1e-8 * abs(cr)
 
 
-def test_stage0_terminal_option_runs():
-    """The reference par path's XT = Q[0] quirk (P:73) is reproducible on request."""
+def test_final_cost_terminal_option_matches_oracle():
+    """terminal="final_cost" (hessian(final_cost) as in the seq path, S:66) instead of the par
+    path's default XT = Q[0] (P:73)."""
     from noc import problems
     from noc.par_interior_point_newton import par_interior_point_optimal_control
     from oracle import noc_oracle as O
@@ -126,9 +127,9 @@ def test_stage0_terminal_option_runs():
     ocp = problems.pendulum(1.0 / N)
     u0 = 0.1 * np.random.default_rng(1).normal(size=(N, 1))
     x0 = np.array([0.1, -0.1])
-    U, it = par_interior_point_optimal_control(ocp, u0, x0, terminal="stage0")
+    U, it = par_interior_point_optimal_control(ocp, u0, x0, terminal="final_cost")
     prob = _oracle_problem("pendulum", N)
-    Ur, itr, _ = O.par_interior_point_optimal_control(prob, u0, x0, terminal="stage0")
+    Ur, itr, _ = O.par_interior_point_optimal_control(prob, u0, x0, terminal="final_cost")
     assert it == itr
     assert np.max(np.abs(U - Ur)) < 1e-6
 
@@ -218,3 +219,32 @@ def test_linear8_ipm_uses_group_solve_and_is_exact():
         _, du, _ = O.dense_kkt(A, B, Q, R, np.zeros((N, 8, 4)), np.zeros((N, 4)),
                                np.diag(fam.wf), 0.0, x0[b])
         assert np.max(np.abs(U[b] - du)) < 1e-8 * max(1.0, np.abs(du).max())
+
+
+@pytest.mark.parametrize("name,N,par_its,par_solves,seq_its,cost", [
+    ("pendulum", 50, 70, 87, 79, 178.3114456),
+    ("pendulum", 100, 69, 85, 80, 354.2079694),
+    ("cartpole", 50, 88, 129, 124, 1842.144564),
+    ("cartpole", 200, 129, 212, 144, 7341.298845),
+])
+def test_solver_reproduces_survey_restatement_numbers(name, N, par_its, par_solves, seq_its, cost):
+    """Pins the GPU solver (persistent kernel, B = 1, the reference's harness setting) to the
+    numbers SURVEY.md §6 measured with an independent fp64 restatement of S and P: outer
+    iterations, KKT solves and the final cost at bp = 0 (u0 = 0.1 N(0,1), numpy seed 1; x0 as
+    PR:90 / CR:101; Ts N = 1 s)."""
+    from noc import problems
+    from noc.par_interior_point_newton import par_interior_point_optimal_control
+    from noc.seq_interior_point_newton import seq_interior_point_optimal_control
+    from noc.utils import wrap_angle
+    ocp = problems.pendulum(1.0 / N) if name == "pendulum" else problems.cartpole(1.0 / N)
+    x0 = (np.array([0.1, -0.1]) if name == "pendulum"
+          else np.array([0.01, float(wrap_angle(-0.01)), 0.01, -0.01]))
+    u0 = 0.1 * np.random.default_rng(1).normal(size=(N, 1))
+    U, it, info = par_interior_point_optimal_control(ocp, u0, x0, return_info=True)
+    assert (it, info["kkt_solves"]) == (par_its, par_solves)
+    prob = _oracle_problem(name, N)
+    from oracle import noc_oracle as O
+    c = prob.total_cost(O.rollout(prob.dynamics, U, x0), U, 0.0)
+    assert abs(c - cost) <= 1e-6 * abs(cost)
+    Us, its = seq_interior_point_optimal_control(ocp, u0, x0)
+    assert its == seq_its
