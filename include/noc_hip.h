@@ -179,6 +179,10 @@ int noc_ipm_promote(const noc_ipm_ws* ws, void* stream);
  * reaches max_solves KKT solves stops with phase != NOC_PHASE_DONE.  On return (stream order)
  * u, x, bp, rp, r_inc, cost, hu, it, total_it, kkt_solves and phase hold the final state. */
 int noc_ipm_solve_supported(const noc_family* fam, int N, int lanes);
+/* Timing-only: per-phase cycle counters of the persistent solver's workgroup 0 (rollout,
+ * linearise, costate + blocks, KKT scan, trial, Newton iterations); all zero unless the library
+ * was built with -DNOC_PERSIST_PROFILE.  reset != 0 zeroes them after reading.  Synchronous. */
+int noc_debug_phase_cycles(long long* out, int n, int reset);
 int noc_ipm_solve(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, double bp0,
                   int max_solves, void* stream);
 

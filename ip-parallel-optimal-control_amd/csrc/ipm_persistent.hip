@@ -24,6 +24,11 @@
 
 namespace noc {
 
+// Per-phase cycle counters of workgroup 0 (timing-only instrumentation; built only with
+// -DNOC_PERSIST_PROFILE, read back by noc_debug_phase_cycles): rollout, linearise, costate +
+// blocks, KKT scan, trial, number of Newton iterations.
+__device__ long long g_phase_cycles[8];
+
 namespace {
 constexpr int PL = 64;  // lanes per trajectory in the persistent solver
 
@@ -41,6 +46,12 @@ NOC_DEV IpmState* state_slot(int N) {
   return reinterpret_cast<IpmState*>(noc_smem + ((N * kd_width<NX, NU>() + NX + 1) & ~1));
 }
 }  // namespace
+
+#ifdef NOC_PERSIST_PROFILE
+#define NOC_PHASE(i) do { const long long t_ = clock64(); if (b == 0 && l == 0) g_phase_cycles[i] += t_ - t_prev; t_prev = t_; } while (0)
+#else
+#define NOC_PHASE(i) do { } while (0)
+#endif
 
 template <int KIND, int NX, int NU>
 __global__ __launch_bounds__(64, 2) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
@@ -73,6 +84,9 @@ __global__ __launch_bounds__(64, 2) void ipm_solve_kernel(noc_family prm, noc_ip
   int it = 0, inner = 0, total_it = 0, solves = 0;
   bool capped = false;
 
+#ifdef NOC_PERSIST_PROFILE
+  long long t_prev = clock64();
+#endif
   for (;;) {  // ---------------- barrier stages (P:228-254) ----------------
     // rollout x_{k+1} = f(x_k, u_k) (noc/utils.py:57-63, P:133): every lane runs the recurrence
     // redundantly with u_k broadcast by readlane; lane t stores the states of block step t
@@ -101,6 +115,7 @@ __global__ __launch_bounds__(64, 2) void ipm_solve_kernel(noc_family prm, noc_ip
       }
     }
     wave_fence();  // states of every stage visible to their chunk owners
+    NOC_PHASE(0);
     bool relinearize = true;
     bool stage_done = false;
     while (!stage_done) {  // ---------------- Newton iterations (P:127-225) ----------------
@@ -121,6 +136,7 @@ __global__ __launch_bounds__(64, 2) void ipm_solve_kernel(noc_family prm, noc_ip
           const double lc = f.stage_cost(x, u, bp);
           tstore<1, PL>(w.lc, b, j, l, cmax, &lc);
         }
+        NOC_PHASE(1);
         // costates as a reverse affine scan (C:34-54) fused with the LQ blocks (P:31-42)
         const double* xN = X + (size_t)N * NX;
         double lamN[NX];
@@ -252,6 +268,7 @@ __global__ __launch_bounds__(64, 2) void ipm_solve_kernel(noc_family prm, noc_ip
       } else {
         w.reg[b] = (mode == NOC_MODE_PAR) ? rp * gnorm : rp;
       }
+      NOC_PHASE(2);
       wave_fence();  // the terminal Hessian (stage-0 lane) and the blocks before the scan
       {  // park the state (every lane stores the same values)
         IpmState* st = state_slot<NX, NU>(N);
@@ -270,6 +287,7 @@ __global__ __launch_bounds__(64, 2) void ipm_solve_kernel(noc_family prm, noc_ip
       }
       const double pred = w.pred[b];
       const bool bwd_ok = w.feasible[b] != 0;
+      NOC_PHASE(3);
       // ---------------- trial point (P:156-175 / S:121-161) ----------------
       double tsum = 0.0;
       int ok = 1;
@@ -315,6 +333,10 @@ __global__ __launch_bounds__(64, 2) void ipm_solve_kernel(noc_family prm, noc_ip
         if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) X[(size_t)N * NX + i] += slot[N * KD + i];
       }
       __syncthreads();  // the next KKT solve overwrites the LDS slots read above
+      NOC_PHASE(4);
+#ifdef NOC_PERSIST_PROFILE
+      if (b == 0 && l == 0) g_phase_cycles[5] += 1;
+#endif
       solves += 1;
       it += end_iter ? 1 : 0;
       if (stop) {                                               // barrier stage finished
@@ -368,6 +390,17 @@ static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, in
   hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU>), dim3(w.Bt), dim3(64), lds, s, p, w, mode,
                      terminal, bp0, max_solves);
   return hipGetLastError();
+}
+
+int debug_phase_cycles(long long* out, int n, int reset) {
+  long long host[8];
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase_cycles), sizeof(host)) != hipSuccess) return -1;
+  for (int i = 0; i < n && i < 8; ++i) out[i] = host[i];
+  if (reset) {
+    const long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), zero, sizeof(zero)) != hipSuccess) return -1;
+  }
+  return 0;
 }
 
 bool ipm_solve_supported(const noc_family& p, int N, int lanes) {

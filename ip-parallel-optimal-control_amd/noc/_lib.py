@@ -71,6 +71,7 @@ SIGNATURES.update({
     "noc_ipm_step_main": (_i, [_fp, _wp, _i, _i, _dp]),
     "noc_ipm_promote": (_i, [_wp, _dp]),
     "noc_ipm_solve_supported": (_i, [_fp, _i, _i]),
+    "noc_debug_phase_cycles": (_i, [ctypes.POINTER(ctypes.c_longlong), _i, _i]),
     "noc_ipm_solve": (_i, [_fp, _wp, _i, _i, ctypes.c_double, _i, _dp]),
 })
 

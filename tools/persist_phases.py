@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""Per-phase cycle breakdown of the persistent solver for one trajectory (B = 1) -- needs the
+library built with -DNOC_PERSIST_PROFILE (load it via NOC_HIP_LIB).  One JSON line per config."""
+import ctypes, json, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ip-parallel-optimal-control_amd"))
+import numpy as np, torch
+from noc import problems, _lib
+from noc.ipm import BatchedIPM
+lib = _lib.load()
+names = ["rollout", "linearize", "costate_blocks", "kkt", "trial", "iterations"]
+for name, N, B in [("pendulum", 50, 1), ("cartpole", 200, 1), ("cartpole", 200, 4096)]:
+    ocp = problems.make_problem(name, N)
+    x0, u0 = problems.initial_conditions(name, N, B, seed=11)
+    eng = BatchedIPM(ocp.family, N, B, persistent=True)
+    eng.load(u0, x0); eng.solve(); torch.cuda.synchronize()
+    buf = (ctypes.c_longlong * 8)()
+    lib.noc_debug_phase_cycles(buf, 8, 1)
+    eng.load(u0, x0)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(); eng.solve(); e1.record(); torch.cuda.synchronize()
+    lib.noc_debug_phase_cycles(buf, 8, 1)
+    c = {k: int(buf[i]) for i, k in enumerate(names)}
+    its = max(c["iterations"], 1)
+    print(json.dumps({"problem": name, "N": N, "B": B, "ms": e0.elapsed_time(e1),
+                      "cycles_per_iteration": {k: c[k] / its for k in names[:5]}, "totals": c}), flush=True)
