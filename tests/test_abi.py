@@ -112,3 +112,37 @@ def test_product_path_fails_loudly_without_gpu():
                       torch.ones(1, 5, 1, 1, dtype=torch.float64),
                       torch.zeros(1, 5, 4, 1, dtype=torch.float64),
                       torch.zeros(1, 5, 1, dtype=torch.float64), torch.eye(4, dtype=torch.float64)[None])
+
+
+def test_persistent_solve_and_grouped_layout_queries_without_gpu():
+    """Capability queries and argument errors of the persistent solver / grouped layout are host
+    logic: checked here without a launch."""
+    from noc import _lib, problems
+    lib = _lib.load()
+    cart = problems.cartpole(0.005).family.to_c()
+    lin8 = problems.double_integrators(4, 0.001).family.to_c()
+    assert lib.noc_ipm_solve_supported(ctypes.byref(cart), 200, 64) == 1
+    assert lib.noc_ipm_solve_supported(ctypes.byref(cart), 1000, 64) == 1   # 40 KB of LDS
+    assert lib.noc_ipm_solve_supported(ctypes.byref(cart), 2000, 64) == 0   # > 64 KB
+    assert lib.noc_ipm_solve_supported(ctypes.byref(cart), 200, 32) == 0    # needs lanes 64
+    assert lib.noc_ipm_solve_supported(ctypes.byref(lin8), 512, 64) == 0    # nx = 8: launch loop
+    # grouped layout (lanes 1) sizes: whole records of 8 trajectories
+    assert lib.noc_tiled_doubles(10, 9, 1, 36) == 16 * 10 * 36
+    assert lib.noc_tiled_doubles(10, 16, 1, 64) == 16 * 10 * 64
+    assert lib.noc_kkt_default_lanes(8, 4, 512) == 1
+    # the grouped tiled layout is only for nx = 8 (before any launch)
+    rc = lib.noc_kkt_solve_tiled(4, 1, 10, 8, 1, *([16] * 6), None, None, 16, None, None, None,
+                                 None, 16, 16, 16, 16, 16, 16, None, None, None)
+    assert rc < 0 and b"grouped" in lib.noc_last_error()
+    # persistent solve argument errors are reported, not launched
+    ws = _lib.NocIpmWs()
+    ws.Bt, ws.N, ws.lanes = 4, 200, 32
+    for f in _lib.WS_DOUBLE_FIELDS + _lib.WS_INT_FIELDS + _lib.WS_STATE_FIELDS:
+        setattr(ws, f, 16)
+    rc = lib.noc_ipm_solve(ctypes.byref(cart), ctypes.byref(ws), 0, 0, 0.1, 100, None)
+    assert rc < 0 and b"lanes = 64" in lib.noc_last_error()
+    ws.lanes = 64
+    rc = lib.noc_ipm_solve(ctypes.byref(cart), ctypes.byref(ws), 0, 0, -1.0, 100, None)
+    assert rc < 0 and b"bp0" in lib.noc_last_error()
+    rc = lib.noc_ipm_solve(ctypes.byref(cart), ctypes.byref(ws), 0, 0, 0.1, 0, None)
+    assert rc < 0 and b"max_solves" in lib.noc_last_error()
