@@ -1,4 +1,4 @@
-"""Compare the persistent and the multi-launch drivers' workspaces after k KKT solves (debug tool:
+"""Debug tool: compare the persistent and the multi-launch drivers' workspaces after k KKT solves."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ip-parallel-optimal-control_amd"))
