@@ -46,7 +46,9 @@ int noc_kkt_default_lanes(int nx, int nu, int N);
  * between its backward and forward phases, so K and d may be passed as NULL. */
 int noc_kkt_gains_on_chip(int nx, int nu, int N, int lanes);
 /* Timing-only phase ablation of the KKT scan (bit0: skip the cross-lane scan, bit1: skip the
- * forward pass, bit2: stop after the in-chunk elements).  Results are WRONG while set; used by
+ * forward pass, bit2: stop after the in-chunk elements, bit3: stream the chunk from memory in
+ * every phase instead of the register-cached chunk; bit 3 alone keeps results exact).  Results of
+ * bits 0-2 are WRONG while set; used by
  * tools/kkt_ablate.py to attribute kernel time to phases.  0 (default) in every product call. */
 void noc_debug_set_ablation(int bits);
 

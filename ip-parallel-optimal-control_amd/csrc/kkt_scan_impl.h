@@ -366,7 +366,11 @@ struct ArgsSrc {
 // The whole KKT solve of trajectory `traj` by lane `l` of its L-lane segment (the kernel below;
 // also called by the persistent interior-point solver, ipm_persistent.hip).  With lds_out set and
 // dx = du = NULL the step stays in the LDS slots (x_s at slot s, u_s after it, x_N at slot N).
-template <int NX, int NU, int L, bool AFF, bool TILED, class SRC>
+// CACHE > 0 (caller guarantees every chunk has <= CACHE stages): the lane's chunk is loaded into
+// registers once, all loads issued up front, and phases 1, 3 and 4 read it from there -- one pass
+// over the blocks and one exposed memory latency instead of three dependent load chains (small
+// nx with one- or two-stage chunks, c2).
+template <int NX, int NU, int L, bool AFF, bool TILED, class SRC, int CACHE = 0>
 NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, const SRC& src) {
   constexpr int KD = kd_width<NX, NU>();
   if (traj >= a.B) return;                     // uniform over the segment
@@ -379,7 +383,13 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   const double reg = a.reg ? a.reg[traj] : 0.0;
   const size_t tN = (size_t)traj * N;
   const int cmax = base + (rem ? 1 : 0);
-
+  StageData<NX, NU> cache[CACHE > 0 ? CACHE : 1];
+  if constexpr (CACHE > 0) {
+    if (a.mode != MODE_FWD) {
+      NOC_UNROLL for (int jj = 0; jj < CACHE; ++jj)
+        if (jj < len) src.stage(start + jj, jj, reg, cache[jj]);
+    }
+  }
 
   Mat<NX, NX> Phi;
   Vec<NX> phi;
@@ -398,10 +408,15 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       set_zero(e.nu);
       set_zero(e.J);
     }
-    for (int s = start + len - 1; s >= start; --s) {
-      StageData<NX, NU> st;
-      src.stage(s, s - start, reg, st);
-      prepend<NX, NU, AFF>(e, st);
+    if constexpr (CACHE > 0) {
+      NOC_UNROLL for (int jj = CACHE - 1; jj >= 0; --jj)
+        if (jj < len) prepend<NX, NU, AFF>(e, cache[jj]);
+    } else {
+      for (int s = start + len - 1; s >= start; --s) {
+        StageData<NX, NU> st;
+        src.stage(s, s - start, reg, st);
+        prepend<NX, NU, AFF>(e, st);
+      }
     }
     // ---------------- phase 2: reverse Hillis-Steele across lanes ----------------
     if (!(a.ablate & 1)) {
@@ -430,9 +445,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     double pred = 0.0;
     int feas = 1;
     double* skd = lds_slots<NX, NU, L>(N);  // K, d stay on chip for phase 4 when staged
-    for (int s = start + len - 1; s >= start; --s) {
-      StageData<NX, NU> st;
-      src.stage(s, s - start, reg, st);
+    auto riccati_stage = [&](const int s, const StageData<NX, NU>& st) {
       Mat<NX, NX> SA;
       Mat<NX, NU> SB;
       NOC_UNROLL for (int i = 0; i < NX; ++i) {
@@ -537,6 +550,16 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
         }
       }
       Phi = Pn;
+    };
+    if constexpr (CACHE > 0) {
+      NOC_UNROLL for (int jj = CACHE - 1; jj >= 0; --jj)
+        if (jj < len) riccati_stage(start + jj, cache[jj]);
+    } else {
+      for (int s = start + len - 1; s >= start; --s) {
+        StageData<NX, NU> st;
+        src.stage(s, s - start, reg, st);
+        riccati_stage(s, st);
+      }
     }
     // segment reductions: pred = sum, feasible = and
     NOC_UNROLL for (int off = L / 2; off > 0; off >>= 1) {
@@ -640,14 +663,8 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       load_Kd<NX, NU, L, TILED>(a, traj, tN + s, s - start, l, cmax, nK);
     }
   };
-  if (len > 0) fetch(start);
-  for (int s = start; s < start + len; ++s) {
-    const Mat<NX, NX> A = nA;
-    const Mat<NX, NU> Bm = nB;
-    const Vec<NX> cc = nc;
-    double Kk[NU * (NX + 1)];
-    NOC_UNROLL for (int i = 0; i < NU * (NX + 1); ++i) Kk[i] = nK[i];
-    if (s + 1 < start + len) fetch(s + 1);  // prefetch the next stage
+  auto fwd_stage = [&](const int s, const Mat<NX, NX>& A, const Mat<NX, NU>& Bm, const Vec<NX>& cc,
+                       const double* Kk) {
     Vec<NU> u;
     NOC_UNROLL for (int i = 0; i < NU; ++i) {
       double t = Kk[NU * NX + i];
@@ -669,6 +686,37 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       xn[i] = t;
     }
     x = xn;
+  };
+  bool from_cache = false;
+  if constexpr (CACHE > 0) from_cache = a.mode != MODE_FWD;
+  if (from_cache) {
+    if constexpr (CACHE > 0) {
+      NOC_UNROLL for (int jj = 0; jj < CACHE; ++jj) {
+        if (jj < len) {
+          const int s = start + jj;
+          double Kk[NU * (NX + 1)];
+          if (kd_lds) {
+            NOC_UNROLL for (int i = 0; i < NU * (NX + 1); ++i) Kk[i] = slot[s * KD + i];
+          } else {
+            load_Kd<NX, NU, L, TILED>(a, traj, tN + s, jj, l, cmax, Kk);
+          }
+          Vec<NX> cc;
+          if constexpr (AFF) cc = cache[jj].c; else set_zero(cc);
+          fwd_stage(s, cache[jj].A, cache[jj].B, cc, Kk);
+        }
+      }
+    }
+  } else {
+    if (len > 0) fetch(start);
+    for (int s = start; s < start + len; ++s) {
+      const Mat<NX, NX> A = nA;
+      const Mat<NX, NU> Bm = nB;
+      const Vec<NX> cc = nc;
+      double Kk[NU * (NX + 1)];
+      NOC_UNROLL for (int i = 0; i < NU * (NX + 1); ++i) Kk[i] = nK[i];
+      if (s + 1 < start + len) fetch(s + 1);  // prefetch the next stage
+      fwd_stage(s, A, Bm, cc, Kk);
+    }
   }
   if (!via_lds) {
     if (last && a.dx) gstore<NX>(a.dx + (tN + traj + N) * NX, x.v);
@@ -701,18 +749,23 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   }
 }
 
-template <int NX, int NU, int L, bool AFF, bool TILED>
+template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE = 0>
 NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
   const int cmax = a.N / L + (a.N % L ? 1 : 0);
   const ArgsSrc<NX, NU, L, AFF, TILED> src{a, traj, l, cmax, (size_t)traj * a.N};
-  kkt_scan_wave_src<NX, NU, L, AFF, TILED>(a, traj, l, src);
+  kkt_scan_wave_src<NX, NU, L, AFF, TILED, ArgsSrc<NX, NU, L, AFF, TILED>, CACHE>(a, traj, l, src);
 }
 
-template <int NX, int NU, int L, bool AFF, bool TILED>
+template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE>
 __global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  kkt_scan_wave<NX, NU, L, AFF, TILED>(a, tid / L, tid % L);
+  kkt_scan_wave<NX, NU, L, AFF, TILED, CACHE>(a, tid / L, tid % L);
 }
+
+// Register-cached chunk length for (NX, NU, L): only where a short chunk's blocks fit beside the
+// scan element (nx = 2: 17 doubles per stage) and the lane count makes chunks short.
+template <int NX, int NU, int L>
+constexpr int kkt_cache_len() { return (NX <= 2 && L >= 32) ? 2 : 0; }
 
 
 
@@ -726,10 +779,20 @@ static hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
   const size_t lds = (a.mode == MODE_BWD || (!a.dx && !a.du)) ? 0 : kkt_lds_bytes_rt(NX, NU, a.N, L);
   a.lds_out = lds > 0 ? 1 : 0;
   if (!a.lds_out && (!a.K || !a.d)) return hipErrorInvalidValue;  // K/d needed as workspace
-  if (a.tiled)
-    hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true>), dim3(grid), dim3(block), lds, stream, a);
-  else
-    hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, false>), dim3(grid), dim3(block), lds, stream, a);
+  constexpr int CC = kkt_cache_len<NX, NU, L>();
+  const int cmax = a.N / L + (a.N % L ? 1 : 0);
+  const bool cached = CC > 0 && cmax <= CC && !(a.ablate & 8);  // ablation bit 3: streamed chunks
+  if (cached) {
+    if (a.tiled)
+      hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, CC>), dim3(grid), dim3(block), lds, stream, a);
+    else
+      hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, false, CC>), dim3(grid), dim3(block), lds, stream, a);
+  } else {
+    if (a.tiled)
+      hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, 0>), dim3(grid), dim3(block), lds, stream, a);
+    else
+      hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, false, 0>), dim3(grid), dim3(block), lds, stream, a);
+  }
   return hipGetLastError();
 }
 
