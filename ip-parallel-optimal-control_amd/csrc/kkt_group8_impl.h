@@ -3,8 +3,10 @@
 // Same algorithm and lane mapping as kkt_group_kernel (kkt_group_impl.h: 8 trajectories per wave,
 // lane q of a group owns state column q), but the backward sweep is latency-hidden: while stage s
 // is computed from LDS buffer s&1, `global_load_lds_dwordx4` (no VGPR destination) streams stage
-// s-1's blocks of the wave's 8 trajectories into the other buffer (13.25 KB: A 4 KB, B 2 KB, Q 4 KB,
-// R 1 KB, M 2 KB, r 256 B).  Lanes then read operands from LDS.  The LDS image of A, B, Q, R is
+// s-1's blocks of the wave's 8 trajectories into the other buffer (grouped layout 9.1 KB: A 4 KB,
+// B 2 KB, packed Q 2.25 KB, packed R 640 B, r 256 B; two buffers = 18.25 KB, so 8 waves fit a CU's
+// 160 KB).  Lanes then read operands from LDS.  M is not staged: lane q needs only its row M[q, :]
+// (32 contiguous bytes), which is prefetched one stage ahead into registers instead.  The LDS image of A, B, Q, R is
 // row-rotated by the trajectory's slot g in the wave (row k of trajectory g stored at row slot
 // (k + g) mod rows), chosen on the SOURCE address of the DMA, so the column reads A[:, q] of the
 // 8 groups fall into different bank quarters (2-way instead of 8-way conflicts).
@@ -14,7 +16,8 @@
 // Two input layouts: natural (the ABI's [b][k][...]; each trajectory's 512/256/128 B blocks are
 // N*sz apart) and grouped (tiled with lanes = 1, small_linalg.h group_base: the wave's 8
 // trajectories of one stage contiguous per field, Q/R packed) -- what the IPM linearisation writes
-// for nx = 8.  Measured c4: grouped 5.69 ms, natural 6.24 ms.
+// for nx = 8.  Measured c4 (grouped): 5.69 ms with M staged in LDS (7 waves/CU), 4.78 ms with the
+// M row loaded per lane (8 waves/CU).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -34,8 +37,8 @@ template <bool TILED>
 struct Lds {
   static constexpr int QB = TILED ? 288 : 512;  // bytes of Q per trajectory
   static constexpr int RB = TILED ? 80 : 128;   // bytes of R per trajectory
-  static constexpr int OA = 0, OB = 4096, OQ = 6144, OR = OQ + 8 * QB, OM = OR + 8 * RB,
-                       ORV = OM + 2048, OC = ORV + 256, OQV = OC + 512;
+  static constexpr int OA = 0, OB = 4096, OQ = 6144, OR = OQ + 8 * QB, ORV = OR + 8 * RB,
+                       OC = ORV + 256, OQV = OC + 512;
   static constexpr int BUF_PLAIN = OC;        // A..r
   static constexpr int BUF_AFF = OQV + 512;   // + c, q
 };
@@ -72,7 +75,7 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
   using LD = Lds<TILED>;
   constexpr int G = NX;
   constexpr int BUF = AFF ? LD::BUF_AFF : LD::BUF_PLAIN;
-  constexpr int OA = LD::OA, OB = LD::OB, OQ = LD::OQ, OR = LD::OR, OM = LD::OM, ORV = LD::ORV,
+  constexpr int OA = LD::OA, OB = LD::OB, OQ = LD::OQ, OR = LD::OR, ORV = LD::ORV,
                 OC = LD::OC, OQV = LD::OQV;
   extern __shared__ __attribute__((aligned(16))) double noc_smem[];
   char* lds = reinterpret_cast<char*>(noc_smem);
@@ -90,16 +93,13 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
 
   if (a.mode != MODE_FWD) {
     // per-lane DMA source offsets (A and Q share theirs; the stage step is uniform)
-    unsigned oA[4], oB[2], oM[2], oQ[4];
+    unsigned oA[4], oB[2], oQ[4];
     NOC_UNROLL for (int i = 0; i < 4; ++i) {
       oA[i] = dma_off(512, 64, 8, i, lane, traj0, a.B, N, TILED);
       // natural Q: full rows, rotated like A; grouped Q: packed (288 B), 3 instructions
       oQ[i] = TILED ? dma_off(LD::QB, LD::QB, 0, i, lane, traj0, a.B, N, true) : oA[i];
     }
-    NOC_UNROLL for (int i = 0; i < 2; ++i) {
-      oB[i] = dma_off(256, 32, 8, i, lane, traj0, a.B, N, TILED);
-      oM[i] = dma_off(256, 32, 0, i, lane, traj0, a.B, N, TILED);
-    }
+    NOC_UNROLL for (int i = 0; i < 2; ++i) oB[i] = dma_off(256, 32, 8, i, lane, traj0, a.B, N, TILED);
     const unsigned oR = TILED ? dma_off(LD::RB, LD::RB, 0, 0, lane < 40 ? lane : 0, traj0, a.B, N, true)
                               : dma_off(128, 32, 4, 0, lane, traj0, a.B, N, false);
     const unsigned orv = dma_off(32, 32, 0, 0, lane < 16 ? lane : 0, traj0, a.B, N, TILED);
@@ -115,7 +115,6 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       const char* bA = ubase(a.A, 512, s);
       const char* bQ = ubase(a.Q, LD::QB, s);
       const char* bB = ubase(a.Bm, 256, s);
-      const char* bM = ubase(a.M, 256, s);
       NOC_UNROLL for (int i = 0; i < 4; ++i) glds16(bA + oA[i], base + OA + i * 1024);
       if constexpr (TILED) {
         glds16(bQ + oQ[0], base + OQ);
@@ -124,10 +123,7 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       } else {
         NOC_UNROLL for (int i = 0; i < 4; ++i) glds16(bQ + oQ[i], base + OQ + i * 1024);
       }
-      NOC_UNROLL for (int i = 0; i < 2; ++i) {
-        glds16(bB + oB[i], base + OB + i * 1024);
-        glds16(bM + oM[i], base + OM + i * 1024);
-      }
+      NOC_UNROLL for (int i = 0; i < 2; ++i) glds16(bB + oB[i], base + OB + i * 1024);
       if (!TILED || lane < 40) glds16(ubase(a.R, LD::RB, s) + oR, base + OR);
       if (lane < 16) glds16(ubase(a.r, 32, s) + orv, base + ORV);
       if constexpr (AFF) {
@@ -151,11 +147,18 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
     if (valid && a.v) a.v[(tN + traj + N) * NX + q] = (AFF && a.p) ? a.p[(size_t)traj * NX + q] : 0.0;
     double pred = 0.0;
     int feas = 1;
+    // row q of M (stage s) straight into registers, one stage ahead like the DMA
+    auto load_mrow = [&](int s, double* m) {
+      const size_t mb = TILED ? group_base(NX * NU, N, trajc, s) : ((size_t)trajc * N + s) * (NX * NU);
+      gload<NU>(a.M + mb + q * NU, m);
+    };
     issue(N - 1, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int s = N - 1; s >= 0; --s) {
       const int buf = (N - 1 - s) & 1;
       if (s > 0) issue(s - 1, buf ^ 1);  // next stage streams in while this one is computed
+      double mrow[NU];
+      load_mrow(s, mrow);  // consumed after the S GEMVs below, which cover most of its latency
       const char* base = lds + buf * BUF;
       // row-rotated LDS images of trajectory g (see header)
       auto Arow = [&](int k) { return reinterpret_cast<const double*>(base + OA + g * 512 + ((k + g) & 7) * 64); };
@@ -169,7 +172,6 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
         if constexpr (TILED) return reinterpret_cast<const double*>(base + OR + g * LD::RB)[Sym<NU>::idx(u, uq)];
         else return reinterpret_cast<const double*>(base + OR + g * 128 + ((u + g) & 3) * 32)[uq];
       };
-      const double* Mg = reinterpret_cast<const double*>(base + OM + g * 256);
       const double* rg = reinterpret_cast<const double*>(base + ORV + g * 32);
       double aq[NX], bq[NX], cc[NX];
       NOC_UNROLL for (int k = 0; k < NX; ++k) {
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       double quc[NU], qux[NU], qu[NU];
       NOC_UNROLL for (int u = 0; u < NU; ++u) {
         quc[u] = Ruq(u) + (u == uq ? reg : 0.0);
-        qux[u] = Mg[q * NU + u];
+        qux[u] = mrow[u];
         qu[u] = rg[u];
       }
       NOC_UNROLL for (int k = 0; k < NX; ++k) {
