@@ -64,9 +64,17 @@ def cpu_baseline(blocks, sample, seconds=10.0, problem="cartpole"):
         kkt_ref.solve(*(host[k] for k in ("A", "B", "Q", "R", "M", "r", "P", "reg")), threads=cores)
         reps += 1
     dt = time.perf_counter() - t0
+    # the survey's 1-core figure: same sample, one thread, a quarter of the time
+    reps1, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < seconds / 4:
+        kkt_ref.solve(*(host[k] for k in ("A", "B", "Q", "R", "M", "r", "P", "reg")), threads=1)
+        reps1 += 1
+    dt1 = time.perf_counter() - t1
     return dict(value=reps * sample / dt, unit="trajectory-KKT-steps/s", cores=cores, kind="port",
+                value_1core=reps1 * sample / dt1,
                 sample=f"{sample} {problem} trajectories x N={host['A'].shape[1]}, {reps} repeats "
-                       f"({dt:.1f} s) of the OpenMP C sequential Riccati (oracle/kkt_ref.c)"), ref
+                       f"({dt:.1f} s) of the OpenMP C sequential Riccati (oracle/kkt_ref.c); "
+                       f"value_1core: {reps1} repeats ({dt1:.1f} s) on one thread"), ref
 
 
 def residual_vs_seq_ref(out, ref, sample):

@@ -16,6 +16,7 @@
 // through the workspace (rollout states, pred / feasible, the terminal Hessian) are ordered by a
 // workgroup fence (one wave = one workgroup).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "../../include/noc_hip.h"
 #include "ipm_family.h"
@@ -53,8 +54,11 @@ NOC_DEV IpmState* state_slot(int N) {
 #define NOC_PHASE(i) do { } while (0)
 #endif
 
-template <int KIND, int NX, int NU>
-__global__ __launch_bounds__(64, 2) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
+// WPS: waves per SIMD the register budget is sized for.  2 = 256 registers per lane; 1 = 512, the
+// upper half AGPRs, which the compiler uses as spill space instead of scratch (cart-pole: 460 B
+// of scratch per lane at WPS = 2, none at WPS = 1).
+template <int KIND, int NX, int NU, int WPS>
+__global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
                                                          int terminal, double bp0,
                                                          int max_solves) {
   const int b = blockIdx.x;  // one wave (= one 64-thread workgroup) per trajectory
@@ -382,12 +386,37 @@ static size_t solve_lds_bytes(int nx, int nu, int N) {
   return bytes <= 65536 ? bytes : 0;
 }
 
+// SIMDs of the current device (4 per CU); 0 if the query fails
+static int device_simds() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  return 4 * cus;
+}
+
+// Families whose kernel spills at 2 waves per SIMD get a 1-wave-per-SIMD instance, used when the
+// batch fits one wave per SIMD anyway (B <= 4 x CUs: the reference's B = 1 runs, c2-sized
+// batches); larger batches keep 2 waves per SIMD for latency hiding.  NOC_PERSIST_WAVES=1|2
+// overrides the choice (timing experiments).
+template <int KIND>
+constexpr bool spills_at_two_waves() { return KIND == NOC_FAMILY_CARTPOLE; }
+
 template <int KIND, int NX, int NU>
 static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                           double bp0, int max_solves, hipStream_t s) {
   const size_t lds = solve_lds_bytes(NX, NU, w.N);
   if (lds == 0) return hipErrorInvalidValue;  // step does not fit in LDS: use the launch driver
-  hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU>), dim3(w.Bt), dim3(64), lds, s, p, w, mode,
+  if constexpr (spills_at_two_waves<KIND>()) {
+    static const int simds = device_simds();
+    static const char* env = getenv("NOC_PERSIST_WAVES");
+    const bool one = env ? atoi(env) == 1 : (simds > 0 && w.Bt <= simds);
+    if (one) {
+      hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 1>), dim3(w.Bt), dim3(64), lds, s, p, w,
+                         mode, terminal, bp0, max_solves);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 2>), dim3(w.Bt), dim3(64), lds, s, p, w, mode,
                      terminal, bp0, max_solves);
   return hipGetLastError();
 }
