@@ -223,6 +223,38 @@ def test_kkt_without_gains_matches_oracle(nx, nu, N, lanes, affine):
     assert np.array_equal(res.feasible.cpu().numpy().astype(bool), ref["feasible"].astype(bool))
 
 
+@pytest.mark.parametrize("N,lanes", [(64, 64), (100, 64), (128, 64), (64, 32), (65, 32)])
+@pytest.mark.parametrize("affine", [False, True])
+@pytest.mark.parametrize("gains", [False, True])
+def test_register_cached_chunk_equals_streamed(N, lanes, affine, gains):
+    """nx = 2 with chunks of <= 2 stages runs the register-cached scan (one load pass).  It must
+    match the oracle and be bit-identical to the streamed scan (ablation bit 3 forces the latter;
+    same arithmetic, only where the blocks are read from differs).  N=65/L=32 mixes chunks of 3
+    (streamed: cmax > 2) as the negative control."""
+    from noc import lqt, _lib
+    case = rand_lq(5000 + N + lanes + int(affine), 7, N, 2, 1, affine=affine)
+    ref = oracle_batch(case)
+    g = lambda k: dev(case.get(k))
+    args = (g("A"), g("B"), g("Q"), g("R"), g("M"), g("r"), g("P"))
+    kw = dict(reg=g("reg"), x0=g("x0"), q=g("q"), c=g("c"), p=g("p"), lanes=lanes,
+              want_gains=gains)
+    lib = _lib.load()
+    try:
+        cached = lqt.kkt_solve(*args, **kw)
+        lib.noc_debug_set_ablation(8)
+        streamed = lqt.kkt_solve(*args, **kw)
+    finally:
+        lib.noc_debug_set_ablation(0)
+    torch.cuda.synchronize()
+    for k in ["dx", "du", "pred"]:
+        assert relerr(getattr(cached, k).cpu(), ref[k]) < RTOL, k
+        assert torch.equal(getattr(cached, k), getattr(streamed, k)), k
+    if gains:
+        assert torch.equal(cached.K, streamed.K) and torch.equal(cached.d, streamed.d)
+        assert relerr(cached.K.cpu(), ref["K"]) < RTOL
+    assert torch.equal(cached.feasible, streamed.feasible)
+
+
 def test_group_solve_linear8_blocks_properties():
     """c4 family (four stacked RK4 double integrators, nx=8, nu=4) at N=512 with a reduced batch:
     the horizon-sequential group solve (lanes=1) against the oracle on a sample, dynamics
