@@ -103,7 +103,10 @@ def ipm_solve_rate(problem, N, B, rank):
     from noc.ipm import BatchedIPM, persistent_supported
     ocp = problems.make_problem(problem, N)
     if not persistent_supported(ocp.family, N):
-        return {"skipped": "persistent solve unsupported for this family / horizon"}
+        # c4 (linear8) is LQ-only in the reference (LM:64-84: par_bwd_pass / par_fwd_pass, no
+        # interior-point loop), so its KKT line is already the end-to-end step
+        return {"skipped": "no persistent instance for this family / horizon (c4 is LQ-only in "
+                           "the reference: one KKT solve per MPC step, LM:67-84)"}
     x0, u0 = problems.initial_conditions(problem, N, B, seed=11 + rank)
     eng = BatchedIPM(ocp.family, N, B, persistent=True)
     eng.load(u0, x0)
