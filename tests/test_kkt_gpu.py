@@ -281,6 +281,37 @@ def test_group_solve_linear8_blocks_properties():
     assert bool(torch.all(res.feasible == 1))
 
 
+@pytest.mark.parametrize("name,N,B,lanes", [("linear8", 512, 16384, 1), ("cartpole", 200, 65536, 32)])
+def test_full_size_bench_blocks_properties(name, N, B, lanes):
+    """The bench path at BASELINE full sizes where the oracle cannot run on every trajectory:
+    c4 (linear8, N=512, B=16384, group solve on the grouped layout) and c5's global batch on ONE
+    GPU (cart-pole, N=200, B=65536 = 8 x 8192: 64-bit indexing of the tiled layout).  Properties:
+    dx_{k+1} = A dx_k + B du_k on every trajectory, all feasible, finite pred, and oracle parity
+    on a strided sample of 8 trajectories including the last one."""
+    from noc import lqt
+    from noc.problems import make_bench_blocks
+    blocks = make_bench_blocks(name, N=N, batch=B, seed=5, lanes=lanes)
+    res = lqt.kkt_solve_tiled(blocks["tiled"], reg=blocks["reg"], want_gains=False)
+    torch.cuda.synchronize()
+    nat = blocks["engine"].natural_blocks()
+    dx, du = res.dx, res.du
+    scale = max(1.0, dx.abs().max().item())
+    for lo in range(0, B, 4096):  # chunked: the einsum temporaries stay small
+        hi = lo + 4096
+        pred_dx = torch.einsum("bkij,bkj->bki", nat["A"][lo:hi], dx[lo:hi, :-1]) + \
+            torch.einsum("bkij,bkj->bki", nat["B"][lo:hi], du[lo:hi])
+        assert (pred_dx - dx[lo:hi, 1:]).abs().max().item() <= 1e-12 * scale, lo
+    assert bool(torch.all(res.feasible == 1))
+    assert bool(torch.all(torch.isfinite(res.pred)))
+    sample = list(range(0, B, B // 8))[:7] + [B - 1]
+    case = {k: nat[k][sample].cpu().numpy() for k in ["A", "B", "Q", "R", "M", "r", "P"]}
+    case["reg"] = blocks["reg"][sample].cpu().numpy()
+    ref = oracle_batch(case)
+    assert relerr(dx[sample].cpu(), ref["dx"]) < RTOL
+    assert relerr(du[sample].cpu(), ref["du"]) < RTOL
+    assert relerr(res.pred[sample].cpu(), ref["pred"]) < RTOL
+
+
 def _lm_lqt(T):
     """examples/linear_mpc_parallel.py:24-64: RK4 double integrator (step 0.001), Q = P =
     diag(1e2, 1), R = 0.1, tracking zero."""
