@@ -56,7 +56,7 @@ NOC_DEV IpmState* state_slot(int N) {
 
 // WPS: waves per SIMD the register budget is sized for.  2 = 256 registers per lane; 1 = 512, the
 // upper half AGPRs, which the compiler uses as spill space instead of scratch (cart-pole: 460 B
-// of scratch per lane at WPS = 2, none at WPS = 1).
+// of scratch per lane at WPS = 2, none at WPS = 1), and which pays for the stage pairs below.
 template <int KIND, int NX, int NU, int WPS>
 __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
                                                          int terminal, double bp0,
@@ -70,6 +70,13 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
   const Chunks ch(N, PL);
   const int start = ch.start(l), len = ch.len(l), cmax = ch.cmax;
   const bool last = (l == PL - 1);
+  // Stage pairs: two stages per pass through the per-stage loops (linearise, costate + blocks,
+  // trial), both loaded before either is computed, so their independent transcendental chains
+  // (sincos, divisions, log) interleave.  Needs the 1-wave-per-SIMD register budget; the trip
+  // count follows the wave-uniform chunk bound cmax (lanes past their own chunk compute a clamped
+  // duplicate stage and discard it).
+  const bool pair = (WPS == 1) && cmax >= 2;
+  auto clampk = [&](int k) { return k < N - 1 ? k : N - 1; };
   double* X = w.x + (size_t)b * (N + 1) * NX;
   double* U = w.u + (size_t)b * N * NU;
   double* LAM = w.lam + (size_t)b * (N + 1) * NX;
@@ -125,20 +132,44 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
     while (!stage_done) {  // ---------------- Newton iterations (P:127-225) ----------------
       if (relinearize) {
         // linearise the own chunk (P:13-28): A = fx, B = fu, cx, cu, stage cost
-        for (int j = 0; j < len; ++j) {
-          const int k = start + j;
-          double x[NX], u[NU];
+        struct LinOut {
+          double fx[NX * NX], fu[NX * NU], cx[NX], cu[NU], lc;
+        };
+        auto lin_compute = [&](const double* x, const double* u, LinOut& o) {
+          f.jac(x, u, o.fx, o.fu);
+          f.stage_grad(x, u, bp, o.cx, o.cu);
+          o.lc = f.stage_cost(x, u, bp);
+        };
+        auto lin_store = [&](int j, const LinOut& o) {
+          tstore<NX * NX, PL>(w.A, b, j, l, cmax, o.fx);
+          tstore<NX * NU, PL>(w.B, b, j, l, cmax, o.fu);
+          tstore<NX, PL>(w.cx, b, j, l, cmax, o.cx);
+          tstore<NU, PL>(w.cu, b, j, l, cmax, o.cu);
+          tstore<1, PL>(w.lc, b, j, l, cmax, &o.lc);
+        };
+        auto load_xu = [&](int k, double* x, double* u) {
           gload<NX>(X + (size_t)k * NX, x);
           NOC_UNROLL for (int i = 0; i < NU; ++i) u[i] = U[(size_t)k * NU + i];
-          double fx[NX * NX], fu[NX * NU], cx[NX], cu[NU];
-          f.jac(x, u, fx, fu);
-          f.stage_grad(x, u, bp, cx, cu);
-          tstore<NX * NX, PL>(w.A, b, j, l, cmax, fx);
-          tstore<NX * NU, PL>(w.B, b, j, l, cmax, fu);
-          tstore<NX, PL>(w.cx, b, j, l, cmax, cx);
-          tstore<NU, PL>(w.cu, b, j, l, cmax, cu);
-          const double lc = f.stage_cost(x, u, bp);
-          tstore<1, PL>(w.lc, b, j, l, cmax, &lc);
+        };
+        if (pair) {  // loads, then both computations, then the stores: one basic block of work
+          for (int j = 0; j < cmax; j += 2) {
+            double x0[NX], u0[NU], x1[NX], u1[NU];
+            load_xu(clampk(start + j), x0, u0);
+            load_xu(clampk(start + j + 1), x1, u1);
+            LinOut o0, o1;
+            lin_compute(x0, u0, o0);
+            lin_compute(x1, u1, o1);
+            if (j < len) lin_store(j, o0);
+            if (j + 1 < len) lin_store(j + 1, o1);
+          }
+        } else {
+          for (int j = 0; j < len; ++j) {
+            double x[NX], u[NU];
+            load_xu(start + j, x, u);
+            LinOut o;
+            lin_compute(x, u, o);
+            lin_store(j, o);
+          }
         }
         NOC_PHASE(1);
         // costates as a reverse affine scan (C:34-54) fused with the LQ blocks (P:31-42)
@@ -200,52 +231,87 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = lamN[i];
         if (last) gstore<NX>(LAM + (size_t)N * NX, lamN);
         double csum = 0.0, hmax = 0.0, g2s = 0.0;
-        for (int j = len - 1; j >= 0; --j) {
-          const int k = start + j;
-          double A[NX * NX], Bm[NX * NU], cx[NX], cu[NU], lc, rr[NU];
-          tload<NX * NX, PL>(w.A, b, j, l, cmax, A);
-          tload<NX * NU, PL>(w.B, b, j, l, cmax, Bm);
-          tload<NX, PL>(w.cx, b, j, l, cmax, cx);
-          tload<NU, PL>(w.cu, b, j, l, cmax, cu);
-          tload<1, PL>(w.lc, b, j, l, cmax, &lc);
-          // LQ blocks at lambda_{k+1} (P:35-37): Q = cxx + l.fxx, R = cuu + l.fuu, M = cxu + l.fxu
-          {
-            double x[NX], u[NU];
-            gload<NX>(X + (size_t)k * NX, x);
-            NOC_UNROLL for (int i = 0; i < NU; ++i) u[i] = U[(size_t)k * NU + i];
-            double Q[NX * NX], R[NU * NU], M[NX * NU];
-            NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int jj = 0; jj < NX; ++jj) Q[i * NX + jj] = (i == jj) ? prm.wx[i] : 0.0;
-            NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int jj = 0; jj < NU; ++jj) R[i * NU + jj] = (i == jj) ? f.stage_cuu(u, bp, i) : 0.0;
-            NOC_UNROLL for (int i = 0; i < NX * NU; ++i) M[i] = 0.0;
-            f.add_hess_l(x, u, lam, Q, R, M);
-            Sym<NX> Qs;
-            Sym<NU> Rs;
-            NOC_UNROLL for (int i = 0; i < NX; ++i)
-              NOC_UNROLL for (int jj = i; jj < NX; ++jj) Qs(i, jj) = (i == jj) ? Q[i * NX + i] : 0.5 * (Q[i * NX + jj] + Q[jj * NX + i]);
-            NOC_UNROLL for (int i = 0; i < NU; ++i)
-              NOC_UNROLL for (int jj = i; jj < NU; ++jj) Rs(i, jj) = (i == jj) ? R[i * NU + i] : 0.5 * (R[i * NU + jj] + R[jj * NU + i]);
-            tstore<Sym<NX>::SZ, PL>(w.Q, b, j, l, cmax, Qs.v);
-            tstore<Sym<NU>::SZ, PL>(w.R, b, j, l, cmax, Rs.v);
-            tstore<NX * NU, PL>(w.M, b, j, l, cmax, M);
-            if (terminal == NOC_TERMINAL_STAGE0 && k == 0) gstore<NX * NX>(w.P + (size_t)b * NX * NX, Q);  // P:73
+        // One stage of the costate sweep fused with its LQ blocks.  `valid` = false computes on a
+        // clamped duplicate stage and leaves lambda, the sums and memory untouched (selects, not
+        // branches, so a pair of stages stays one basic block).
+        struct StageIn {
+          double A[NX * NX], Bm[NX * NU], cx[NX], cu[NU], lc, x[NX], u[NU];
+        };
+        auto load_in = [&](int j, StageIn& in) {
+          // 0 <= j < cmax: every lane's tiled slots exist up to cmax; for a slot past the lane's
+          // own chunk the data are a discarded duplicate (x, u clamped into the horizon)
+          tload<NX * NX, PL>(w.A, b, j, l, cmax, in.A);
+          tload<NX * NU, PL>(w.B, b, j, l, cmax, in.Bm);
+          tload<NX, PL>(w.cx, b, j, l, cmax, in.cx);
+          tload<NU, PL>(w.cu, b, j, l, cmax, in.cu);
+          tload<1, PL>(w.lc, b, j, l, cmax, &in.lc);
+          load_xu(clampk(start + j), in.x, in.u);
+        };
+        // LQ blocks at lambda_{k+1} (P:35-37): Q = cxx + l.fxx, R = cuu + l.fuu, M = cxu + l.fxu;
+        // ru_k = cu_k + fu_k' lambda_{k+1} (P:34); then lambda_k = cx_k + fx_k' lambda_{k+1}
+        struct StageOut {
+          Sym<NX> Qs;
+          Sym<NU> Rs;
+          double M[NX * NU], rr[NU], lam[NX];
+        };
+        auto cost_compute = [&](const StageIn& in, bool valid, StageOut& o) {
+          double Q[NX * NX], R[NU * NU];
+          NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int jj = 0; jj < NX; ++jj) Q[i * NX + jj] = (i == jj) ? prm.wx[i] : 0.0;
+          NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int jj = 0; jj < NU; ++jj) R[i * NU + jj] = (i == jj) ? f.stage_cuu(in.u, bp, i) : 0.0;
+          NOC_UNROLL for (int i = 0; i < NX * NU; ++i) o.M[i] = 0.0;
+          f.add_hess_l(in.x, in.u, lam, Q, R, o.M);
+          NOC_UNROLL for (int i = 0; i < NX; ++i)
+            NOC_UNROLL for (int jj = i; jj < NX; ++jj) o.Qs(i, jj) = (i == jj) ? Q[i * NX + i] : 0.5 * (Q[i * NX + jj] + Q[jj * NX + i]);
+          NOC_UNROLL for (int i = 0; i < NU; ++i)
+            NOC_UNROLL for (int jj = i; jj < NU; ++jj) o.Rs(i, jj) = (i == jj) ? R[i * NU + i] : 0.5 * (R[i * NU + jj] + R[jj * NU + i]);
+          NOC_UNROLL for (int jj = 0; jj < NU; ++jj) {
+            double r = in.cu[jj];
+            NOC_UNROLL for (int i = 0; i < NX; ++i) r += in.Bm[i * NU + jj] * lam[i];
+            o.rr[jj] = r;
+            hmax = valid ? fmax(hmax, fabs(r)) : hmax;
+            g2s = valid ? g2s + in.cu[jj] * in.cu[jj] : g2s;
           }
-          NOC_UNROLL for (int jj = 0; jj < NU; ++jj) {  // ru_k = cu_k + fu_k' lambda_{k+1}  (P:34)
-            double r = cu[jj];
-            NOC_UNROLL for (int i = 0; i < NX; ++i) r += Bm[i * NU + jj] * lam[i];
-            rr[jj] = r;
-            hmax = fmax(hmax, fabs(r));
-            g2s += cu[jj] * cu[jj];
-          }
-          tstore<NU, PL>(w.r, b, j, l, cmax, rr);
-          double ln[NX];
           NOC_UNROLL for (int i = 0; i < NX; ++i) {
-            double t = cx[i];
-            NOC_UNROLL for (int m = 0; m < NX; ++m) t += A[m * NX + i] * lam[m];
-            ln[i] = t;
+            double t = in.cx[i];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) t += in.A[m * NX + i] * lam[m];
+            o.lam[i] = t;
           }
-          NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = ln[i];
-          gstore<NX>(LAM + (size_t)k * NX, lam);
-          csum += lc;
+          csum = valid ? csum + in.lc : csum;
+          NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = valid ? o.lam[i] : lam[i];
+        };
+        auto cost_store = [&](int j, const StageIn& in, const StageOut& o) {
+          const int k = start + j;
+          tstore<Sym<NX>::SZ, PL>(w.Q, b, j, l, cmax, o.Qs.v);
+          tstore<Sym<NU>::SZ, PL>(w.R, b, j, l, cmax, o.Rs.v);
+          tstore<NX * NU, PL>(w.M, b, j, l, cmax, o.M);
+          if (terminal == NOC_TERMINAL_STAGE0 && k == 0) {  // XT = Q[0] (P:73), full matrix
+            double Q[NX * NX];
+            NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int jj = 0; jj < NX; ++jj) Q[i * NX + jj] = o.Qs(i, jj);
+            gstore<NX * NX>(w.P + (size_t)b * NX * NX, Q);
+          }
+          tstore<NU, PL>(w.r, b, j, l, cmax, o.rr);
+          gstore<NX>(LAM + (size_t)k * NX, o.lam);
+        };
+        if (pair) {  // descending pairs over the wave-uniform chunk bound; short lanes skip slots
+          for (int j = cmax - 1; j >= 0; j -= 2) {
+            StageIn in0, in1;
+            load_in(j, in0);
+            load_in(j - 1 >= 0 ? j - 1 : j, in1);
+            const bool v0 = j < len, v1 = j - 1 >= 0 && j - 1 < len;
+            StageOut o0, o1;
+            cost_compute(in0, v0, o0);
+            cost_compute(in1, v1, o1);
+            if (v0) cost_store(j, in0, o0);
+            if (v1) cost_store(j - 1, in1, o1);
+          }
+        } else {
+          for (int j = len - 1; j >= 0; --j) {
+            StageIn in;
+            load_in(j, in);
+            StageOut o;
+            cost_compute(in, true, o);
+            cost_store(j, in, o);
+          }
         }
         // lambda at the chunk start := the scan's value g (not this lane's sweep): it is exactly the
         // boundary costate the previous lane used, so every consumer of lambda_k sees one value
@@ -295,13 +361,28 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       // ---------------- trial point (P:156-175 / S:121-161) ----------------
       double tsum = 0.0;
       int ok = 1;
-      for (int j = 0; j < len; ++j) {
-        const int k = start + j;
-        double xt[NX], ut[NU];
+      auto trial_load = [&](int k, double* xt, double* ut) {
         NOC_UNROLL for (int i = 0; i < NX; ++i) xt[i] = X[(size_t)k * NX + i] + slot[k * KD + i];
         NOC_UNROLL for (int jj = 0; jj < NU; ++jj) ut[jj] = U[(size_t)k * NU + jj] + slot[k * KD + NX + jj];
-        ok &= f.feasible(ut) ? 1 : 0;
-        tsum += f.stage_cost(xt, ut, bp);
+      };
+      if (pair) {  // both stages loaded, then both costs; summed in stage order like trial_kernel
+        for (int j = 0; j < cmax; j += 2) {
+          double xt0[NX], ut0[NU], xt1[NX], ut1[NU];
+          trial_load(clampk(start + j), xt0, ut0);
+          trial_load(clampk(start + j + 1), xt1, ut1);
+          const double c0 = f.stage_cost(xt0, ut0, bp);
+          const double c1 = f.stage_cost(xt1, ut1, bp);
+          const bool f0 = f.feasible(ut0), f1 = f.feasible(ut1);
+          if (j < len) { ok &= f0 ? 1 : 0; tsum += c0; }
+          if (j + 1 < len) { ok &= f1 ? 1 : 0; tsum += c1; }
+        }
+      } else {
+        for (int j = 0; j < len; ++j) {
+          double xt[NX], ut[NU];
+          trial_load(start + j, xt, ut);
+          ok &= f.feasible(ut) ? 1 : 0;
+          tsum += f.stage_cost(xt, ut, bp);
+        }
       }
       if (last) {
         double xt[NX];
@@ -394,27 +475,23 @@ static int device_simds() {
   return 4 * cus;
 }
 
-// Families whose kernel spills at 2 waves per SIMD get a 1-wave-per-SIMD instance, used when the
-// batch fits one wave per SIMD anyway (B <= 4 x CUs: the reference's B = 1 runs, c2-sized
-// batches); larger batches keep 2 waves per SIMD for latency hiding.  NOC_PERSIST_WAVES=1|2
-// overrides the choice (timing experiments).
-template <int KIND>
-constexpr bool spills_at_two_waves() { return KIND == NOC_FAMILY_CARTPOLE; }
+// Two instances per family: 1 wave per SIMD (512 registers per lane: no spills, stage pairs) when
+// the batch fits one wave per SIMD anyway (B <= 4 x CUs: the reference's B = 1 runs, c2-sized
+// batches), 2 waves per SIMD above that for latency hiding.  NOC_PERSIST_WAVES=1|2 overrides the
+// choice (timing experiments).
 
 template <int KIND, int NX, int NU>
 static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                           double bp0, int max_solves, hipStream_t s) {
   const size_t lds = solve_lds_bytes(NX, NU, w.N);
   if (lds == 0) return hipErrorInvalidValue;  // step does not fit in LDS: use the launch driver
-  if constexpr (spills_at_two_waves<KIND>()) {
-    static const int simds = device_simds();
-    static const char* env = getenv("NOC_PERSIST_WAVES");
-    const bool one = env ? atoi(env) == 1 : (simds > 0 && w.Bt <= simds);
-    if (one) {
-      hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 1>), dim3(w.Bt), dim3(64), lds, s, p, w,
-                         mode, terminal, bp0, max_solves);
-      return hipGetLastError();
-    }
+  static const int simds = device_simds();
+  static const char* env = getenv("NOC_PERSIST_WAVES");
+  const bool one = env ? atoi(env) == 1 : (simds > 0 && w.Bt <= simds);
+  if (one) {
+    hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 1>), dim3(w.Bt), dim3(64), lds, s, p, w,
+                       mode, terminal, bp0, max_solves);
+    return hipGetLastError();
   }
   hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 2>), dim3(w.Bt), dim3(64), lds, s, p, w, mode,
                      terminal, bp0, max_solves);
