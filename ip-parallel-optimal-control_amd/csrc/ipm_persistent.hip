@@ -475,23 +475,28 @@ static int device_simds() {
   return 4 * cus;
 }
 
-// Two instances per family: 1 wave per SIMD (512 registers per lane: no spills, stage pairs) when
-// the batch fits one wave per SIMD anyway (B <= 4 x CUs: the reference's B = 1 runs, c2-sized
-// batches), 2 waves per SIMD above that for latency hiding.  NOC_PERSIST_WAVES=1|2 overrides the
-// choice (timing experiments).
+// Families whose kernel spills at 2 waves per SIMD (cart-pole) get a second instance at 1 wave per
+// SIMD (512 registers per lane: no scratch, stage pairs), used when the batch fits one wave per
+// SIMD anyway (B <= 4 x CUs: the reference's B = 1 runs, c2-sized batches); larger batches keep 2
+// waves per SIMD for latency hiding.  The others stay at 2 waves (their 1-wave instance measured
+// 5-7 % slower at B = 1).  NOC_PERSIST_WAVES=1|2 overrides the choice (timing experiments).
+template <int KIND>
+constexpr bool one_wave_instance() { return KIND == NOC_FAMILY_CARTPOLE; }
 
 template <int KIND, int NX, int NU>
 static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                           double bp0, int max_solves, hipStream_t s) {
   const size_t lds = solve_lds_bytes(NX, NU, w.N);
   if (lds == 0) return hipErrorInvalidValue;  // step does not fit in LDS: use the launch driver
-  static const int simds = device_simds();
-  static const char* env = getenv("NOC_PERSIST_WAVES");
-  const bool one = env ? atoi(env) == 1 : (simds > 0 && w.Bt <= simds);
-  if (one) {
-    hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 1>), dim3(w.Bt), dim3(64), lds, s, p, w,
-                       mode, terminal, bp0, max_solves);
-    return hipGetLastError();
+  if constexpr (one_wave_instance<KIND>()) {
+    static const int simds = device_simds();
+    static const char* env = getenv("NOC_PERSIST_WAVES");
+    const bool one = env ? atoi(env) == 1 : (simds > 0 && w.Bt <= simds);
+    if (one) {
+      hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 1>), dim3(w.Bt), dim3(64), lds, s, p, w,
+                         mode, terminal, bp0, max_solves);
+      return hipGetLastError();
+    }
   }
   hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 2>), dim3(w.Bt), dim3(64), lds, s, p, w, mode,
                      terminal, bp0, max_solves);
