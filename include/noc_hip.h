@@ -188,6 +188,20 @@ int noc_debug_phase_cycles(long long* out, int n, int reset);
 int noc_ipm_solve(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, double bp0,
                   int max_solves, void* stream);
 
+/* Interior-point DDP (noc/differential_dynamic_programming.py: interior_point_ddp, D:189-208):
+ * the whole barrier schedule of DDP iterations (second-order backward pass with the Vx . fxx
+ * terms, nonlinear closed-loop rollout, retry loop) of every trajectory in ONE launch, one lane
+ * per trajectory.  Natural layout: x0 (Bt, nx), u (Bt, N, nu) = initial controls on entry, final
+ * controls on return.  work: noc_ddp_work_doubles(nx, nu, N, Bt) doubles (on return it starts
+ * with the final states (Bt, N+1, nx)).  iterations[b] = total DDP iterations (the reference's
+ * return value), passes[b] = backward passes incl. rejected retries, done[b] = 0 if max_passes
+ * stopped the trajectory early.  Families with nx <= 4 (noc_ddp_supported). */
+long long noc_ddp_work_doubles(int nx, int nu, int N, int Bt);
+int noc_ddp_supported(const noc_family* fam);
+int noc_ddp_solve(const noc_family* fam, int N, int Bt, const double* x0, double* u, double* work,
+                  int* iterations, int* passes, int* done, double bp0, int max_passes,
+                  void* stream);
+
 #ifdef __cplusplus
 }
 #endif

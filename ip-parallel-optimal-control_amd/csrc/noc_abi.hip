@@ -310,6 +310,34 @@ int noc_ipm_solve(const noc_family* fam, const noc_ipm_ws* ws, int mode, int ter
                                    static_cast<hipStream_t>(stream)), "ipm_solve");
 }
 
+long long noc_ddp_work_doubles(int nx, int nu, int N, int Bt) {
+  if (nx < 1 || nu < 1 || N < 1 || Bt < 0) return -1;
+  const long long b = Bt, n = N;
+  return b * (2 * (n + 1) * nx + 2 * n * nu + n * nu * nx);  // X, TX, TU, k, K
+}
+
+int noc_ddp_supported(const noc_family* fam) { return (fam && noc::ddp_supported(*fam)) ? 1 : 0; }
+
+int noc_ddp_solve(const noc_family* fam, int N, int Bt, const double* x0, double* u, double* work,
+                  int* iterations, int* passes, int* done, double bp0, int max_passes,
+                  void* stream) {
+  if (!fam) return fail(-2, "family is NULL");
+  if (!noc::ddp_supported(*fam))
+    return fail(-1, "DDP supports the registered families with nx <= 4 (noc_ddp_supported)");
+  if (N < 1) return fail(-1, "horizon N must be >= 1");
+  if (Bt < 0) return fail(-1, "batch Bt must be >= 0");
+  if (!(bp0 > 0.0)) return fail(-1, "bp0 must be > 0");
+  if (max_passes < 1) return fail(-1, "max_passes must be >= 1");
+  int rc = 0;
+  if ((rc = check_ptr(x0, "x0", true)) || (rc = check_ptr(u, "u", true)) ||
+      (rc = check_ptr(work, "work", true)) || (rc = check_ptr(iterations, "iterations", true)) ||
+      (rc = check_ptr(passes, "passes", true)) || (rc = check_ptr(done, "done", true)))
+    return rc;
+  if (Bt == 0) return 0;
+  return hip_status(noc::ddp_solve(*fam, N, Bt, x0, u, work, iterations, passes, done, bp0,
+                                   max_passes, static_cast<hipStream_t>(stream)), "ddp_solve");
+}
+
 static int kkt_and_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* stream) {
   // the trial step needs dx, du only: gains stay on chip when they fit (ws->K, ws->d otherwise)
   const bool on_chip = noc_kkt_gains_on_chip(fam->nx, fam->nu, ws->N, ws->lanes) == 1;

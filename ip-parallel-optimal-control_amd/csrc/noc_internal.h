@@ -49,6 +49,11 @@ hipError_t ipm_promote(const noc_ipm_ws& w, hipStream_t s);
 hipError_t ipm_init(const noc_ipm_ws& w, double bp0, hipStream_t s);
 // persistent whole-solve kernel (ipm_persistent.hip)
 bool ipm_solve_supported(const noc_family& p, int N, int lanes);
+// interior-point DDP (ddp_persistent.hip)
+bool ddp_supported(const noc_family& p);
+hipError_t ddp_solve(const noc_family& p, int N, int Bt, const double* x0, double* u,
+                     double* work, int* iterations, int* passes, int* done, double bp0,
+                     int max_passes, hipStream_t s);
 int debug_phase_cycles(long long* out, int n, int reset);
 hipError_t ipm_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal, double bp0,
                      int max_solves, hipStream_t s);

@@ -73,6 +73,9 @@ SIGNATURES.update({
     "noc_ipm_solve_supported": (_i, [_fp, _i, _i]),
     "noc_debug_phase_cycles": (_i, [ctypes.POINTER(ctypes.c_longlong), _i, _i]),
     "noc_ipm_solve": (_i, [_fp, _wp, _i, _i, ctypes.c_double, _i, _dp]),
+    "noc_ddp_work_doubles": (ctypes.c_longlong, [_i, _i, _i, _i]),
+    "noc_ddp_supported": (_i, [_fp]),
+    "noc_ddp_solve": (_i, [_fp, _i, _i] + [_dp] * 6 + [ctypes.c_double, _i, _dp]),
 })
 
 _lib: Optional[ctypes.CDLL] = None

@@ -10,7 +10,7 @@ from-scratch associative-scan restatement of paroc's par_bwd_pass/par_fwd_pass),
 tests/test_oracle.py.
 
 Abbreviations: S = noc/seq_interior_point_newton.py, P = noc/par_interior_point_newton.py,
-C = noc/costates.py, U = noc/utils.py.
+C = noc/costates.py, U = noc/utils.py, D = noc/differential_dynamic_programming.py.
 
 LQ sub-problem conventions (shared with the HIP kernel, include/noc_hip.h)
 -------------------------------------------------------------------------
@@ -413,3 +413,101 @@ def par_interior_point_optimal_control(prob, U, x0, terminal="final_cost"):
         total += it
         solves += s
     return U, total, solves
+
+
+# ----------------------------------------------------------------------------------------------
+# interior-point DDP (D:28-208): sequential second-order backward pass + nonlinear rollout
+# ----------------------------------------------------------------------------------------------
+def ddp_bwd_pass(Vx_T, Vxx_T, derivs, reg_param):
+    """D:28-70.  reg = reg_param * ||cu||_F; Q-function with the second-order dynamics terms
+    Vx . fxx (tensordot over the output axis); eigh(Quu) > 0 feasibility; LU solves.
+    Returns (ffgain k (N,nu), gain K (N,nu,nx), pred_reduction, feasible, Hu = Qu (N,nu))."""
+    cx, cu, cxx, cuu, cxu, fx, fu, fxx, fuu, fxu = derivs
+    N, nu = cu.shape
+    nx = cx.shape[1]
+    reg = reg_param * float(np.linalg.norm(cu))                         # D:34-35
+    Vx, Vxx = np.asarray(Vx_T, dtype=np.float64), np.asarray(Vxx_T, dtype=np.float64)
+    k = np.zeros((N, nu))
+    K = np.zeros((N, nu, nx))
+    Hu = np.zeros((N, nu))
+    dV = np.zeros(N)
+    feasible = True
+    for t in range(N - 1, -1, -1):                                      # lax.scan(reverse=True)
+        Qx = cx[t] + fx[t].T @ Vx                                       # D:41
+        Qu = cu[t] + fu[t].T @ Vx                                       # D:42
+        Qxx = cxx[t] + fx[t].T @ Vxx @ fx[t] + np.tensordot(Vx, fxx[t], axes=1)   # D:43
+        Qxu = cxu[t] + fx[t].T @ Vxx @ fu[t] + np.tensordot(Vx, fxu[t], axes=1)   # D:44
+        Quu = cuu[t] + fu[t].T @ Vxx @ fu[t] + np.tensordot(Vx, fuu[t], axes=1)   # D:45
+        Quu = Quu + reg * np.eye(nu)                                    # D:46
+        feasible &= bool(np.all(np.linalg.eigvalsh(Quu) > 0))           # D:47-48
+        k[t] = -np.linalg.solve(Quu, Qu)                                # D:50
+        K[t] = -np.linalg.solve(Quu, Qxu.T)                             # D:51
+        dV[t] = -0.5 * Qu @ np.linalg.solve(Quu, Qu)                    # D:53
+        Vx = Qx - Qu @ np.linalg.solve(Quu, Qxu.T)                      # D:54
+        Vxx = Qxx - Qxu @ np.linalg.solve(Quu, Qxu.T)                   # D:55
+        Hu[t] = Qu
+    return k, K, float(dV.sum()), feasible, Hu                          # D:61-70
+
+
+def ddp_nonlin_rollout(prob, K, k, X, U):
+    """D:73-90: u_hat = u + k + K (x_hat - x); x_hat+ = f(x_hat, u_hat) from x_hat_0 = x_0."""
+    N = U.shape[0]
+    TX = np.zeros_like(X)
+    TU = np.zeros_like(U)
+    xh = X[0].copy()
+    for t in range(N):
+        uh = U[t] + k[t] + K[t] @ (xh - X[t])
+        TX[t], TU[t] = xh, uh
+        xh = prob.dynamics(xh, uh)
+    TX[N] = xh
+    return TX, TU
+
+
+def ddp(prob, U, x0, bp, trace=None):
+    """D:98-186.  Quirk kept: inside one inner (retry) loop the failure multiplier is the OUTER
+    iteration's reg_inc (D:132 closes over it), while r_inc doubles per failure and becomes the
+    next outer iteration's reg_inc (D:133, D:154).  The last trial is kept even if the retry cap
+    ended the inner loop (D:154).  Returns (X, U, iterations, bwd passes)."""
+    X = rollout(prob.dynamics, U, x0)                                   # D:102
+    reg_param, reg_inc = 1.0, 2.0                                       # D:102-103
+    it, passes, Hu_norm = 0, 0, 1.0
+    while not (Hu_norm < 1e-4 or it > 500):                             # D:167-170
+        cost = prob.total_cost(X, U, bp)                                # D:109
+        derivs = prob.derivatives(X, U, bp)                             # D:112
+        Vx_T, Vxx_T = prob.final_grad_hess(X[-1])                       # D:58-59
+        rp, r_inc, inner = reg_param, reg_inc, 0
+        while True:
+            k, K, pred, feas, Hu = ddp_bwd_pass(Vx_T, Vxx_T, derivs, rp)
+            passes += 1
+            TX, TU = ddp_nonlin_rollout(prob, K, k, X, U)
+            Hn = float(np.max(np.abs(Hu)))
+            new_cost = prob.total_cost(TX, TU, bp) if prob.feasible(TX, TU) else np.inf
+            with np.errstate(all="ignore"):
+                gain = (new_cost - cost) / pred
+            success = bool(gain > 0) and feas                          # D:128
+            if success:
+                rp = rp * max(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) ** 3)
+                r_inc = 2.0
+            else:
+                rp = rp * reg_inc                                       # outer reg_inc (D:132)
+                r_inc = 2 * r_inc
+            rp = min(max(rp, 1e-16), 1e16)                              # D:135
+            inner += 1
+            if trace is not None:
+                trace.append(dict(it=it, inner=inner, pred=pred, gain=gain, success=success, rp=rp))
+            if success or inner > 500:                                  # D:147-152
+                break
+        X, U, Hu_norm, reg_param, reg_inc = TX, TU, Hn, rp, r_inc       # D:154-162
+        it += 1
+    return X, U, it, passes
+
+
+def interior_point_ddp(prob, U, x0):
+    """D:189-208: barrier 0.1 / 5^k while bp > 1e-4.  Returns (U*, total iterations, passes)."""
+    bp, total, passes = 0.1, 0, 0
+    while bp > 1e-4:
+        _, U, it, p = ddp(prob, U, x0, bp)
+        bp /= 5
+        total += it
+        passes += p
+    return U, total, passes

@@ -146,3 +146,26 @@ def test_persistent_solve_and_grouped_layout_queries_without_gpu():
     assert rc < 0 and b"bp0" in lib.noc_last_error()
     rc = lib.noc_ipm_solve(ctypes.byref(cart), ctypes.byref(ws), 0, 0, 0.1, 0, None)
     assert rc < 0 and b"max_solves" in lib.noc_last_error()
+
+
+def test_ddp_queries_and_argument_errors_without_gpu():
+    """noc_ddp_*: workspace size, family support (nx <= 4) and argument validation are host logic."""
+    from noc import _lib, problems
+    lib = _lib.load()
+    assert lib.noc_ddp_work_doubles(4, 1, 200, 3) == 3 * (2 * 201 * 4 + 2 * 200 + 200 * 4)
+    assert lib.noc_ddp_work_doubles(0, 1, 10, 1) < 0
+    for ocp, ok in ((problems.pendulum(0.02), 1), (problems.cartpole(0.005), 1),
+                    (problems.double_integrators(1, 0.1), 1),
+                    (problems.double_integrators(4, 0.001), 0)):
+        assert lib.noc_ddp_supported(ctypes.byref(ocp.family.to_c())) == ok
+    pend = problems.pendulum(0.02).family.to_c()
+    args = [16, 16, 16, 16, 16, 16]  # 16-byte aligned fake device addresses: never dereferenced
+    assert lib.noc_ddp_solve(None, 10, 1, *args, 0.1, 10, None) == -2
+    assert lib.noc_ddp_solve(ctypes.byref(pend), 0, 1, *args, 0.1, 10, None) < 0
+    assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 1, *args, 0.0, 10, None) < 0
+    assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 1, *args, 0.1, 0, None) < 0
+    assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 1, None, *args[1:], 0.1, 10, None) == -2
+    assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 0, *args, 0.1, 10, None) == 0  # empty batch
+    lin8 = problems.double_integrators(4, 0.001).family.to_c()
+    assert lib.noc_ddp_solve(ctypes.byref(lin8), 10, 1, *args, 0.1, 10, None) < 0
+    assert b"nx <= 4" in lib.noc_last_error()

@@ -8,8 +8,8 @@ warm-up call, then 10 timed calls of the par and seq interior-point solves, each
 device sync (the reference's jax.block_until_ready); mean and median per (Ts, N) written to CSV
 files named like the reference's (<problem>_ip_means_par.csv, ..._medians_seq.csv; one column,
 pandas layout).  Differences: u0 comes from numpy default_rng(1) (jax.random.PRNGKey(1) is not
-available here); interior-point DDP is out of scope, so no *_ddp.csv; `--batch B`
-optionally solves B copies at once (B = 1 is the reference's setting).
+available here); `--batch B` optionally solves B copies at once (B = 1 is the reference's
+setting).  All three solvers the reference times: par, seq and interior-point DDP (*_ddp.csv).
 
 Usage: python tools/runtime_sweep.py [--problem pendulum|cartpole] [--out DIR] [--runs 10]
 """
@@ -41,10 +41,12 @@ def main():
     from noc import problems
     from noc.par_interior_point_newton import par_interior_point_optimal_control
     from noc.seq_interior_point_newton import seq_interior_point_optimal_control
+    from noc.differential_dynamic_programming import interior_point_ddp
     from noc.utils import wrap_angle
 
     os.makedirs(args.out, exist_ok=True)
-    stats = {k: [] for k in ("par_mean", "par_median", "seq_mean", "seq_median")}
+    stats = {k: [] for k in ("par_mean", "par_median", "seq_mean", "seq_median", "ddp_mean",
+                             "ddp_median")}
     rows = []
     for ts, n in zip(TS, NS):
         if n > args.max_n:
@@ -60,7 +62,8 @@ def main():
             x0 = np.repeat(x0[None], args.batch, 0)
         res = {}
         for tag, fn in (("par", par_interior_point_optimal_control),
-                        ("seq", seq_interior_point_optimal_control)):
+                        ("seq", seq_interior_point_optimal_control),
+                        ("ddp", interior_point_ddp)):
             out = fn(ocp, u, x0)          # warm-up (the reference's first jitted call)
             torch.cuda.synchronize()
             times = []
@@ -77,7 +80,7 @@ def main():
         rows.append({"Ts": ts, "N": n, "batch": args.batch, **res})
         print(json.dumps(rows[-1]), flush=True)
     p = args.problem
-    for tag in ("par", "seq"):
+    for tag in ("par", "seq", "ddp"):
         pd.DataFrame(np.array(stats[f"{tag}_mean"])).to_csv(os.path.join(args.out, f"{p}_ip_means_{tag}.csv"))
         pd.DataFrame(np.array(stats[f"{tag}_median"])).to_csv(os.path.join(args.out, f"{p}_ip_medians_{tag}.csv"))
     with open(os.path.join(args.out, f"{p}_runtime.json"), "w") as fh:
