@@ -190,8 +190,8 @@ int noc_ipm_solve(const noc_family* fam, const noc_ipm_ws* ws, int mode, int ter
 
 /* Interior-point DDP (noc/differential_dynamic_programming.py: interior_point_ddp, D:189-208):
  * the whole barrier schedule of DDP iterations (second-order backward pass with the Vx . fxx
- * terms, nonlinear closed-loop rollout, retry loop) of every trajectory in ONE launch, one lane
- * per trajectory.  Natural layout: x0 (Bt, nx), u (Bt, N, nu) = initial controls on entry, final
+ * terms, nonlinear closed-loop rollout, retry loop) of every trajectory in ONE launch, one wave64
+ * per trajectory (stage derivatives lane-parallel, the recursions wave-uniform).  Natural layout: x0 (Bt, nx), u (Bt, N, nu) = initial controls on entry, final
  * controls on return.  work: noc_ddp_work_doubles(nx, nu, N, Bt) doubles (on return it starts
  * with the final states (Bt, N+1, nx)).  iterations[b] = total DDP iterations (the reference's
  * return value), passes[b] = backward passes incl. rejected retries, done[b] = 0 if max_passes

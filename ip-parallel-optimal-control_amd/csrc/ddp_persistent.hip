@@ -1,17 +1,24 @@
 // Interior-point DDP on the MI355X: the reference's third solver
 // (noc/differential_dynamic_programming.py, "D"), the whole barrier schedule of every trajectory
-// in ONE launch.
+// in ONE launch, one wave64 per trajectory.
 //
 // DDP's backward pass is NOT the KKT scan: its Q-function carries the second-order dynamics terms
 // Vx . fxx evaluated with the pass's own value gradient Vx_{k+1} (D:43-45), so the recursion is
 // nonlinear in V and has no associative form; the forward pass is the nonlinear closed-loop
-// rollout (D:73-90).  Both are horizon-sequential per trajectory, so the mapping is one lane per
-// trajectory: the stage derivatives are evaluated on the fly from the nominal (x, u) (the same
-// sympy-generated family code as the Newton solvers; Vx . fxx is add_hess_l with l = Vx), nothing
-// is materialised but the gains k, K and the trial trajectory.  Every lane runs its own reference
-// control flow (outer Newton loop D:105-170, retry loop D:114-152, barrier loop D:189-208).
-// Layout: natural, per trajectory contiguous (x (Bt, N+1, nx), u (Bt, N, nu)); workspace
-// include/noc_hip.h noc_ddp_work_doubles.
+// rollout (D:73-90).  Both recursions are horizon-sequential.  What is NOT sequential is the
+// expensive part of a backward step -- the stage derivatives at the nominal (x, u) (the generated
+// family code: sincos, divisions), which are the same for every retry of an iteration.  So:
+//   * derivatives: the 64 lanes evaluate them stage-parallel once per DDP iteration into a
+//     per-stage record (fx, fu, cx, cu, cuu and the full second-derivative tensors d2f_i, taken
+//     as add_hess_l with l = e_i), written to HBM / L2;
+//   * backward pass: wave-uniform (every lane runs the same recursion; lane 0 stores k, K),
+//     reading the records -- only the Vx contraction and the Riccati-like algebra remain;
+//   * rollouts: wave-uniform recurrence (lane 0 stores), then trial cost and feasibility
+//     stage-parallel with wave reductions (cost summed chunk-wise in stage order, then across
+//     lanes: the summation order of the multi-lane Newton kernels).
+// Every wave follows its own trajectory's reference control flow (outer Newton loop D:105-170,
+// retry loop D:114-152, barrier loop D:189-208).  Layout: natural, per trajectory contiguous
+// (x (Bt, N+1, nx), u (Bt, N, nu)); workspace include/noc_hip.h noc_ddp_work_doubles.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -27,63 +34,114 @@ struct DdpArgs {
   double bp0;
   const double* x0;
   double* u;
-  double *X, *TX, *TU, *k, *K;
+  double *X, *TX, *TU, *k, *K, *rec;
   int *iterations, *passes, *done;
 };
 
+// per-stage derivative record: fx | fu | cx | cu | cuu (diagonal) | Hxx_i | Hxu_i | Huu_i (i < nx)
+template <int NX, int NU>
+struct Rec {
+  static constexpr int FX = 0, FU = FX + NX * NX, CX = FU + NX * NU, CU = CX + NX, CUU = CU + NU,
+                       HXX = CUU + NU, HXU = HXX + NX * NX * NX, HUU = HXU + NX * NX * NU,
+                       SIZE = HUU + NX * NU * NU;
+};
+
+NOC_DEV void ddp_fence() { __threadfence_block(); }  // this wave's global stores before its loads
+
 template <int KIND, int NX, int NU>
 __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  using R = Rec<NX, NU>;
+  const int b = blockIdx.x;  // one wave per trajectory
+  const int l = threadIdx.x;
   if (b >= a.Bt) return;
   const Fam<KIND, NX, NU> f(prm);
   const int N = a.N;
-  double* ubuf = a.u + (size_t)b * N * NU;
+  const Chunks ch(N, 64);
+  const int start = ch.start(l), len = ch.len(l);
+  double* const ubuf = a.u + (size_t)b * N * NU;
+  double* const xbuf = a.X + (size_t)b * (N + 1) * NX;
   double* U = ubuf;
   double* TU = a.TU + (size_t)b * N * NU;
-  double* X = a.X + (size_t)b * (N + 1) * NX;
+  double* X = xbuf;
   double* TX = a.TX + (size_t)b * (N + 1) * NX;
   double* kk = a.k + (size_t)b * N * NU;
   double* KK = a.K + (size_t)b * N * NU * NX;
+  double* rec = a.rec + (size_t)b * N * R::SIZE;
   const double* x0 = a.x0 + (size_t)b * NX;
+  const bool lead = (l == 0);
 
-  // ocp.total_cost (PR:53-56 / CR:48-51): stage costs in stage order, then the final cost
-  auto total_cost = [&](const double* Xs, const double* Us, double bp) {
+  // ocp.total_cost (PR:53-56 / CR:48-51) and check_feasibility (D:93-95) of (Xs, Us), lane-parallel
+  auto cost_feas = [&](const double* Xs, const double* Us, double bp, bool& feasible) {
     double c = 0.0;
-    for (int t = 0; t < N; ++t) c += f.stage_cost(Xs + (size_t)t * NX, Us + (size_t)t * NU, bp);
-    return c + f.final_cost(Xs + (size_t)N * NX);
+    bool ok = true;
+    for (int t = start; t < start + len; ++t) {
+      ok = ok && f.feasible(Us + (size_t)t * NU);
+      c += f.stage_cost(Xs + (size_t)t * NX, Us + (size_t)t * NU, bp);
+    }
+    feasible = __all(ok);
+    return wave_sum(c) + f.final_cost(Xs + (size_t)N * NX);
   };
 
   double bp = a.bp0;
   int total_it = 0, passes = 0;
   bool capped = false;
   while (bp > 1e-4 && !capped) {  // ---------------- barrier schedule (D:189-208) ----------------
-    // rollout of the current controls (D:101, U:57-63)
+    // rollout of the current controls (D:101, U:57-63): wave-uniform recurrence, lane 0 stores
     {
       double x[NX];
-      NOC_UNROLL for (int i = 0; i < NX; ++i) { x[i] = x0[i]; X[i] = x[i]; }
+      NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = x0[i];
+      if (lead) NOC_UNROLL for (int i = 0; i < NX; ++i) X[i] = x[i];
       for (int t = 0; t < N; ++t) {
         double xn[NX];
         f.step(x, U + (size_t)t * NU, xn);
-        NOC_UNROLL for (int i = 0; i < NX; ++i) { x[i] = xn[i]; X[(size_t)(t + 1) * NX + i] = xn[i]; }
+        NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = xn[i];
+        if (lead) NOC_UNROLL for (int i = 0; i < NX; ++i) X[(size_t)(t + 1) * NX + i] = xn[i];
       }
     }
+    ddp_fence();
     double reg_param = 1.0, reg_inc = 2.0, hu_norm = 1.0;  // D:102-103, D:183
     int it = 0;
     while (!(hu_norm < 1e-4 || it > 500)) {  // ---------------- DDP iterations (D:167-170) -------
-      const double cost = total_cost(X, U, bp);  // D:109
-      // reg = rp * ||cu||_F of the nominal derivatives (D:34-35)
+      bool unused;
+      const double cost = cost_feas(X, U, bp, unused);  // D:109
+      // stage derivatives at the nominal trajectory (D:112), stage-parallel; ||cu||_F (D:34)
       double g2 = 0.0;
-      for (int t = 0; t < N; ++t) {
-        double cx[NX], cu[NU];
-        f.stage_grad(X + (size_t)t * NX, U + (size_t)t * NU, bp, cx, cu);
-        NOC_UNROLL for (int j = 0; j < NU; ++j) g2 += cu[j] * cu[j];
+      for (int t = start; t < start + len; ++t) {
+        const double* x = X + (size_t)t * NX;
+        const double* u = U + (size_t)t * NU;
+        double* r = rec + (size_t)t * R::SIZE;
+        double fx[NX * NX], fu[NX * NU], cx[NX], cu[NU];
+        f.jac(x, u, fx, fu);
+        f.stage_grad(x, u, bp, cx, cu);
+        NOC_UNROLL for (int i = 0; i < NX * NX; ++i) r[R::FX + i] = fx[i];
+        NOC_UNROLL for (int i = 0; i < NX * NU; ++i) r[R::FU + i] = fu[i];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) r[R::CX + i] = cx[i];
+        NOC_UNROLL for (int j = 0; j < NU; ++j) {
+          r[R::CU + j] = cu[j];
+          r[R::CUU + j] = f.stage_cuu(u, bp, j);
+          g2 += cu[j] * cu[j];
+        }
+        if constexpr (KIND != NOC_FAMILY_LINEAR) {  // d2 f_i = add_hess_l with l = e_i
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            double e[NX], hxx[NX * NX], huu[NU * NU], hxu[NX * NU];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) e[m] = (m == i) ? 1.0 : 0.0;
+            NOC_UNROLL for (int m = 0; m < NX * NX; ++m) hxx[m] = 0.0;
+            NOC_UNROLL for (int m = 0; m < NU * NU; ++m) huu[m] = 0.0;
+            NOC_UNROLL for (int m = 0; m < NX * NU; ++m) hxu[m] = 0.0;
+            f.add_hess_l(x, u, e, hxx, huu, hxu);
+            NOC_UNROLL for (int m = 0; m < NX * NX; ++m) r[R::HXX + i * NX * NX + m] = hxx[m];
+            NOC_UNROLL for (int m = 0; m < NX * NU; ++m) r[R::HXU + i * NX * NU + m] = hxu[m];
+            NOC_UNROLL for (int m = 0; m < NU * NU; ++m) r[R::HUU + i * NU * NU + m] = huu[m];
+          }
+        }
       }
-      const double gnorm = sqrt(g2);
+      const double gnorm = sqrt(wave_sum(g2));
+      ddp_fence();
       double rp = reg_param, r_inc = reg_inc, hn = 0.0;
       int inner = 0;
       bool success = false;
       for (;;) {  // ---------------- retry loop (D:114-152) ----------------
-        // backward pass (D:37-70): Vx_N, Vxx_N = grad, hessian of the final cost (D:58-59)
+        // backward pass (D:37-70), wave-uniform: Vx_N, Vxx_N = grad, hessian of the final cost
         const double reg = rp * gnorm;
         double Vx[NX], Vxx[NX * NX];
         {
@@ -97,27 +155,31 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
         bool feas = true;
         hn = 0.0;
         for (int t = N - 1; t >= 0; --t) {
-          double x[NX], u[NU];
-          NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = X[(size_t)t * NX + i];
-          NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = U[(size_t)t * NU + j];
-          double fx[NX * NX], fu[NX * NU], cx[NX], cu[NU];
-          f.jac(x, u, fx, fu);
-          f.stage_grad(x, u, bp, cx, cu);
-          // cxx, cuu, cxu of the stage cost + the Vx-contracted dynamics Hessians (D:43-45)
+          const double* r = rec + (size_t)t * R::SIZE;
+          double fx[NX * NX], fu[NX * NU];
+          NOC_UNROLL for (int i = 0; i < NX * NX; ++i) fx[i] = r[R::FX + i];
+          NOC_UNROLL for (int i = 0; i < NX * NU; ++i) fu[i] = r[R::FU + i];
+          // cxx = diag(wx), cxu = 0, cuu (stage cost); + Vx . d2f (D:43-45)
           double Qxx[NX * NX], Quu[NU * NU], Qxu[NX * NU];
           NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) Qxx[i * NX + j] = (i == j) ? prm.wx[i] : 0.0;
-          NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int j = 0; j < NU; ++j) Quu[i * NU + j] = (i == j) ? f.stage_cuu(u, bp, i) : 0.0;
+          NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int j = 0; j < NU; ++j) Quu[i * NU + j] = (i == j) ? r[R::CUU + i] : 0.0;
           NOC_UNROLL for (int i = 0; i < NX * NU; ++i) Qxu[i] = 0.0;
-          f.add_hess_l(x, u, Vx, Qxx, Quu, Qxu);
+          if constexpr (KIND != NOC_FAMILY_LINEAR) {
+            NOC_UNROLL for (int i = 0; i < NX; ++i) {
+              NOC_UNROLL for (int m = 0; m < NX * NX; ++m) Qxx[m] += Vx[i] * r[R::HXX + i * NX * NX + m];
+              NOC_UNROLL for (int m = 0; m < NX * NU; ++m) Qxu[m] += Vx[i] * r[R::HXU + i * NX * NU + m];
+              NOC_UNROLL for (int m = 0; m < NU * NU; ++m) Quu[m] += Vx[i] * r[R::HUU + i * NU * NU + m];
+            }
+          }
           // Qx = cx + fx'Vx, Qu = cu + fu'Vx (D:41-42); W = Vxx fx, Z = Vxx fu
           double Qx[NX], Qu[NU], W[NX * NX], Z[NX * NU];
           NOC_UNROLL for (int j = 0; j < NX; ++j) {
-            double s = cx[j];
+            double s = r[R::CX + j];
             NOC_UNROLL for (int i = 0; i < NX; ++i) s += fx[i * NX + j] * Vx[i];
             Qx[j] = s;
           }
           NOC_UNROLL for (int j = 0; j < NU; ++j) {
-            double s = cu[j];
+            double s = r[R::CU + j];
             NOC_UNROLL for (int i = 0; i < NX; ++i) s += fu[i * NU + j] * Vx[i];
             Qu[j] = s;
           }
@@ -162,8 +224,10 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
           feas = ldl_solve<NU, NX + 1>(Qs, Y) && feas;
           // k = -Quu^-1 Qu, K = -Quu^-1 Qux (D:50-51); dV = -1/2 Qu'Quu^-1 Qu (D:53)
           NOC_UNROLL for (int i = 0; i < NU; ++i) {
-            kk[(size_t)t * NU + i] = -Y[i][0];
-            NOC_UNROLL for (int j = 0; j < NX; ++j) KK[((size_t)t * NU + i) * NX + j] = -Y[i][1 + j];
+            if (lead) {
+              kk[(size_t)t * NU + i] = -Y[i][0];
+              NOC_UNROLL for (int j = 0; j < NX; ++j) KK[((size_t)t * NU + i) * NX + j] = -Y[i][1 + j];
+            }
             pred += -0.5 * Qu[i] * Y[i][0];
             hn = fmax(hn, fabs(Qu[i]));  // Hu = Qu (D:56, D:120)
           }
@@ -181,10 +245,8 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
             }
         }
         passes += 1;
-        // nonlinear rollout of the closed loop (D:73-90) fused with check_feasibility (D:93-95)
-        // and the trial cost (stage order, then the final cost, like total_cost above)
-        bool ok = true;
-        double tcost = 0.0;
+        ddp_fence();
+        // nonlinear rollout of the closed loop (D:73-90): wave-uniform, lane 0 stores
         {
           double xh[NX];
           NOC_UNROLL for (int i = 0; i < NX; ++i) xh[i] = X[i];
@@ -196,17 +258,19 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
               NOC_UNROLL for (int j = 0; j < NX; ++j) s += KK[((size_t)t * NU + i) * NX + j] * dxh[j];
               uh[i] = s;
             }
-            NOC_UNROLL for (int i = 0; i < NX; ++i) TX[(size_t)t * NX + i] = xh[i];
-            NOC_UNROLL for (int i = 0; i < NU; ++i) TU[(size_t)t * NU + i] = uh[i];
-            ok = ok && f.feasible(uh);
-            tcost += f.stage_cost(xh, uh, bp);
+            if (lead) {
+              NOC_UNROLL for (int i = 0; i < NX; ++i) TX[(size_t)t * NX + i] = xh[i];
+              NOC_UNROLL for (int i = 0; i < NU; ++i) TU[(size_t)t * NU + i] = uh[i];
+            }
             double xn[NX];
             f.step(xh, uh, xn);
             NOC_UNROLL for (int i = 0; i < NX; ++i) xh[i] = xn[i];
           }
-          NOC_UNROLL for (int i = 0; i < NX; ++i) TX[(size_t)N * NX + i] = xh[i];
-          tcost += f.final_cost(xh);
+          if (lead) NOC_UNROLL for (int i = 0; i < NX; ++i) TX[(size_t)N * NX + i] = xh[i];
         }
+        ddp_fence();
+        bool ok;
+        const double tcost = cost_feas(TX, TU, bp, ok);
         const double new_cost = ok ? tcost : INFINITY;             // D:121-125
         const double gain = (new_cost - cost) / pred;               // D:126-127
         success = (gain > 0.0) && feas;                             // D:128
@@ -230,26 +294,28 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
     total_it += it;  // D:196
     bp = bp / 5.0;   // D:195
   }
-  if (U != ubuf) {  // the final controls live in the trial buffer: copy them out
-    for (int t = 0; t < N * NU; ++t) ubuf[t] = U[t];
+  // the final controls / states may live in the trial buffers: copy them out (lane-parallel)
+  if (U != ubuf) for (int i = l; i < N * NU; i += 64) ubuf[i] = U[i];
+  if (X != xbuf) for (int i = l; i < (N + 1) * NX; i += 64) xbuf[i] = X[i];
+  if (lead) {
+    a.iterations[b] = total_it;
+    a.passes[b] = passes;
+    a.done[b] = capped ? 0 : 1;
   }
-  if (X != a.X + (size_t)b * (N + 1) * NX) {  // and the final states into X
-    double* Xo = a.X + (size_t)b * (N + 1) * NX;
-    for (int t = 0; t < (N + 1) * NX; ++t) Xo[t] = X[t];
-  }
-  a.iterations[b] = total_it;
-  a.passes[b] = passes;
-  a.done[b] = capped ? 0 : 1;
 }
 
 template <int KIND, int NX, int NU>
 static hipError_t ddp_t(const noc_family& p, const DdpArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((ddp_solve_kernel<KIND, NX, NU>), dim3((a.Bt + 63) / 64), dim3(64), 0, s, p, a);
+  hipLaunchKernelGGL((ddp_solve_kernel<KIND, NX, NU>), dim3(a.Bt), dim3(64), 0, s, p, a);
   return hipGetLastError();
 }
 
 bool ddp_supported(const noc_family& p) {
-  return family_supported(p) && p.nx <= 4;  // one lane holds the nx x nx value Hessian
+  return family_supported(p) && p.nx <= 4;  // one wave holds the nx x nx value Hessian
+}
+
+long long ddp_record_doubles(int nx, int nu) {
+  return (long long)nx * nx + nx * nu + nx + 2 * nu + (long long)nx * (nx * nx + nx * nu + nu * nu);
 }
 
 hipError_t ddp_solve(const noc_family& p, int N, int Bt, const double* x0, double* u,
@@ -268,6 +334,7 @@ hipError_t ddp_solve(const noc_family& p, int N, int Bt, const double* x0, doubl
   a.TU = a.TX + nxs;
   a.k = a.TU + nus;
   a.K = a.k + nus;
+  a.rec = a.K + nus * p.nx;
   a.iterations = iterations;
   a.passes = passes;
   a.done = done;

@@ -313,7 +313,8 @@ int noc_ipm_solve(const noc_family* fam, const noc_ipm_ws* ws, int mode, int ter
 long long noc_ddp_work_doubles(int nx, int nu, int N, int Bt) {
   if (nx < 1 || nu < 1 || N < 1 || Bt < 0) return -1;
   const long long b = Bt, n = N;
-  return b * (2 * (n + 1) * nx + 2 * n * nu + n * nu * nx);  // X, TX, TU, k, K
+  // X, TX, TU, k, K and the per-stage derivative records
+  return b * (2 * (n + 1) * nx + 2 * n * nu + n * nu * nx + n * noc::ddp_record_doubles(nx, nu));
 }
 
 int noc_ddp_supported(const noc_family* fam) { return (fam && noc::ddp_supported(*fam)) ? 1 : 0; }

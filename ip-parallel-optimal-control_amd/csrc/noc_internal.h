@@ -51,6 +51,7 @@ hipError_t ipm_init(const noc_ipm_ws& w, double bp0, hipStream_t s);
 bool ipm_solve_supported(const noc_family& p, int N, int lanes);
 // interior-point DDP (ddp_persistent.hip)
 bool ddp_supported(const noc_family& p);
+long long ddp_record_doubles(int nx, int nu);
 hipError_t ddp_solve(const noc_family& p, int N, int Bt, const double* x0, double* u,
                      double* work, int* iterations, int* passes, int* done, double bp0,
                      int max_passes, hipStream_t s);

@@ -3,8 +3,9 @@ solver, "D").
 
 `interior_point_ddp(ocp, controls, initial_state) -> (controls*, iterations)` keeps the
 reference signature (D:189-208).  The whole barrier schedule runs on the MI355X in one launch
-(`noc_ddp_solve`, one lane per trajectory: DDP's backward pass carries the Vx . fxx terms of its
-own value gradient, so it is horizon-sequential, not a scan).  Differences, all additive:
+(`noc_ddp_solve`, one wave per trajectory: DDP's backward pass carries the Vx . fxx terms of its
+own value gradient, so the recursion is horizon-sequential, not a scan; the stage derivatives are
+evaluated lane-parallel).  Differences, all additive:
   * inputs may carry a leading batch axis (controls (B, N, nu), initial_state (B, nx)); the
     result is then batched too -- each trajectory follows its own reference control flow;
   * `ocp.family` must be a registered family with nx <= 4 (noc.problems);
