@@ -1,9 +1,9 @@
 #!/bin/bash
 # Profile refresh after the cached-chunk scan (c2) and the 8-waves/CU group solve (c4): GPU tests,
 # kernel traces, HBM PMC passes (FETCH_SIZE and WRITE_SIZE in separate runs) for c2 and c4, and
-# the three bench lines.  Usage (repo root, via gpurun): gpurun --timeout 1200 -- bash tools/gpu_prof_r1d.sh
+# the three bench lines.  Usage (repo root, via gpurun): gpurun --timeout 1200 -- bash tools/gpu_profile.sh
 R="${GRAFT_REPO_ROOT:-/root/repo}"
-cd "$R"; O=gpurun_out/prof_r1d; mkdir -p $O
+cd "$R"; O=gpurun_out/profile; mkdir -p $O
 export TMPDIR=/tmp
 run() { local t=$1; local log=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$log" 2>&1; local rc=$?; echo "rc=$rc $log"; tail -1 "$O/$log" | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi; }
 C2="--problem pendulum --horizon 100 --batch 1024 --steps 50 --warmup 5 --no-cpu --no-ipm"
