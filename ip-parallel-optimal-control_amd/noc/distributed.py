@@ -128,3 +128,33 @@ def solve_sharded(ocp, controls, initial_state, mode=None, terminal=None,
         it = np.zeros(0, dtype=np.int32)
         solves = np.zeros(0, dtype=np.int32)
     return gather_rows(U, B, world), gather_rows(it, B, world), gather_rows(solves, B, world)
+
+
+def ddp_sharded(ocp, controls, initial_state, ddp_fn: Optional[Callable] = None,
+                info: Optional[dict] = None, **kw):
+    """Batched interior-point DDP (noc.differential_dynamic_programming.interior_point_ddp, D:189-208)
+    sharded over the process group like solve_sharded: every rank passes the FULL batch, solves its
+    contiguous slice in one launch, and gets the full (controls*, iterations, passes) back.  No
+    collective on the solve path; `info` receives the global backward-pass total and the number of
+    trajectories a max_passes cap stopped early (two 8-byte all-reduces).  `ddp_fn(ocp, u, x0,
+    return_info=True, **kw) -> (U, its, info)` is injectable for CPU tests."""
+    if ddp_fn is None:
+        from .differential_dynamic_programming import interior_point_ddp as ddp_fn
+    world, rank = dist.get_world_size(), dist.get_rank()
+    u = np.asarray(controls, dtype=np.float64)
+    x0 = np.asarray(initial_state, dtype=np.float64)
+    B = u.shape[0]
+    lo, hi = shard_bounds(B, world, rank)
+    if hi > lo:
+        U, its, inf = ddp_fn(ocp, u[lo:hi], x0[lo:hi], return_info=True, **kw)
+        its = np.asarray(its, dtype=np.int32).reshape(-1)
+        passes = np.asarray(inf["passes"], dtype=np.int32).reshape(-1)
+        capped = int(np.sum(~np.asarray(inf["done"], dtype=bool)))
+    else:
+        U = np.zeros((0,) + u.shape[1:])
+        its = np.zeros(0, dtype=np.int32)
+        passes = np.zeros(0, dtype=np.int32)
+        capped = 0
+    if info is not None:
+        info.update(passes_total=sum_global(int(passes.sum())), not_done=sum_global(capped))
+    return gather_rows(U, B, world), gather_rows(its, B, world), gather_rows(passes, B, world)

@@ -106,3 +106,46 @@ def test_sharded_solve_world2_gloo(B, persistent):
         # the global convergence norm is the all-reduce(MAX) over both ranks' shards
         assert info["convergence_norm"] == pytest.approx(1e-5 * (B - 1))
         assert info["not_done"] == 0
+
+
+def _fake_ddp(ocp, u, x0, return_info=True):
+    """interior_point_ddp stand-in: iterations = 10 + b, passes = 2 (10 + b), u shifted by b."""
+    b = np.round(x0[:, 0]).astype(int)
+    return (u + b[:, None, None], (10 + b).astype(np.int32),
+            dict(passes=(2 * (10 + b)).astype(np.int32), done=b != 3))
+
+
+def _ddp_worker(rank, world, port, B, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from noc import distributed as D
+    u = np.arange(B * 5, dtype=np.float64).reshape(B, 5, 1)
+    x0 = np.zeros((B, 2))
+    x0[:, 0] = np.arange(B)
+    info = {}
+    U, it, passes = D.ddp_sharded(None, u, x0, ddp_fn=_fake_ddp, info=info)
+    q.put((rank, U, it, passes, info))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B", [5, 1])
+def test_ddp_sharded_world2_gloo(B):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    b = np.arange(B)
+    for rank, U, it, passes, info in res:
+        assert np.array_equal(U, np.arange(B * 5, dtype=np.float64).reshape(B, 5, 1) + b[:, None, None])
+        assert np.array_equal(it, 10 + b) and np.array_equal(passes, 2 * (10 + b))
+        assert info["passes_total"] == int(np.sum(2 * (10 + b)))
+        assert info["not_done"] == int(np.sum(b == 3))
