@@ -77,8 +77,10 @@ def _device_problem(name, N):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,N,Bt", [("pendulum", 30, 3), ("cartpole", 25, 2), ("linear2", 20, 2)])
+@pytest.mark.parametrize("name,N,Bt", [("pendulum", 30, 3), ("cartpole", 25, 2), ("linear2", 20, 2),
+                                       ("pendulum", 1, 2), ("pendulum", 130, 1)])
 def test_ddp_matches_oracle(name, N, Bt):
+    """N=1: one stage, 63 idle lanes; N=130: uneven lane chunks (3 / 2 stages)."""
     from noc.differential_dynamic_programming import interior_point_ddp
     from oracle import noc_oracle as O
     rng = np.random.default_rng(7 + N)
