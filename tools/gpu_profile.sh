@@ -20,7 +20,7 @@ run 200 c4_write.log rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/$O/c4
 cp profiles/pmc_traffic.json $O/pmc_traffic.json
 python tools/pmc_traffic.py $O/c2_fetch/run_counter_collection.csv $O/c2_write/run_counter_collection.csv pendulum_N100_B1024 $O/pmc_traffic.json kkt_scan
 python tools/pmc_traffic.py $O/c4_fetch/run_counter_collection.csv $O/c4_write/run_counter_collection.csv linear8_N512_B16384 $O/pmc_traffic.json kkt_group8
-cp $O/pmc_traffic.json profiles/pmc_traffic.json
+# only gpurun_out/ comes back from the box: merge $O/pmc_traffic.json into profiles/pmc_traffic.json by hand
 run 300 bench_c3.log python bench.py
 run 300 bench_c2.log python bench.py --problem pendulum --horizon 100 --batch 1024 --steps 100 --warmup 10 --cpu-seconds 5
 run 300 bench_c4.log python bench.py --problem linear8 --horizon 512 --batch 16384 --lanes 1 --steps 10 --warmup 2 --cpu-seconds 10 --cpu-sample 256
