@@ -24,9 +24,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ip-parallel-optimal-control_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-CONFIG_LABEL = {("cartpole", 200, 4096): "BASELINE c3; c5 when run on 8 GPUs",
+CONFIG_LABEL = {("cartpole", 200, 4096): "BASELINE c3 per GPU; weak scaling over --gpus (c5's 65536 = --batch 8192 on 8 GPUs)",
                 ("pendulum", 100, 1024): "BASELINE c2",
-                ("linear8", 512, 16384): "BASELINE c4"}
+                ("linear8", 512, 16384): "BASELINE c4",
+                ("cartpole", 200, 8192): "BASELINE c5 per-GPU shard (65536 / 8)"}
 
 
 def algorithmic_bytes(nx, nu, N, B):
