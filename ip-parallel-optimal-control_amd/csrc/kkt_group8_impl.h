@@ -67,6 +67,40 @@ NOC_DEV unsigned dma_off(int sz, int rb, int rows, int i, int lane, int traj0, i
 NOC_DEV void glds16(const char* src, char* lds_dst) {
   __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)lds_dst, 16, 0, 0);
 }
+
+#ifndef NOC_G8_DPP
+#define NOC_G8_DPP 1
+#endif
+// Broadcast lane J of every 8-lane group to the whole group on the VALU (DPP row_newbcast: lane n
+// of each 16-lane row to the row; bank_mask 0x3 writes lanes 0-7 of the row from row lane J, 0xC
+// lanes 8-15 from row lane 8+J) instead of a ds_bpermute through the LDS pipe, which the backward
+// sweep saturates (SQ_INSTS_LDS).  Every lane of the wave must be active.
+template <int J>
+NOC_DEV double bcast8(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  int rlo = __builtin_amdgcn_update_dpp(0, lo, 0x150 + J, 0xF, 0x3, false);
+  int rhi = __builtin_amdgcn_update_dpp(0, hi, 0x150 + J, 0xF, 0x3, false);
+  rlo = __builtin_amdgcn_update_dpp(rlo, lo, 0x158 + J, 0xF, 0xC, false);
+  rhi = __builtin_amdgcn_update_dpp(rhi, hi, 0x158 + J, 0xF, 0xC, false);
+  return __hiloint2double(rhi, rlo);
+}
+// group broadcast with a (post-unrolling) constant source lane
+NOC_DEV double gb(double x, int j) {
+#if NOC_G8_DPP
+  switch (j) {
+    case 0: return bcast8<0>(x);
+    case 1: return bcast8<1>(x);
+    case 2: return bcast8<2>(x);
+    case 3: return bcast8<3>(x);
+    case 4: return bcast8<4>(x);
+    case 5: return bcast8<5>(x);
+    case 6: return bcast8<6>(x);
+    default: return bcast8<7>(x);
+  }
+#else
+  return gshfl(x, j, TPW);
+#endif
+}
 }  // namespace g8
 
 template <bool AFF, bool TILED>
@@ -213,7 +247,7 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       }
       Sym<NU> Quu;
       NOC_UNROLL for (int i = 0; i < NU; ++i)
-        NOC_UNROLL for (int j = i; j < NU; ++j) Quu(i, j) = gshfl(quc[i], j, G);
+        NOC_UNROLL for (int j = i; j < NU; ++j) Quu(i, j) = gb(quc[i], j);
       double Y[NU][2];
       NOC_UNROLL for (int u = 0; u < NU; ++u) {
         Y[u][0] = qux[u];
@@ -252,11 +286,11 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
         NOC_UNROLL for (int i = 0; i < NX; ++i) sn[i] += ar[i] * saq[k];
       }
       NOC_UNROLL for (int u = 0; u < NU; ++u) {
-        NOC_UNROLL for (int i = 0; i < NX; ++i) sn[i] += gshfl(qux[u], i, G) * Kq[u];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) sn[i] += gb(qux[u], i) * Kq[u];
       }
       NOC_UNROLL for (int i = 0; i < NX; ++i)
-        NOC_UNROLL for (int j = i; j < NX; ++j) S(i, j) = gshfl(sn[i], j, G);
-      NOC_UNROLL for (int i = 0; i < NX; ++i) v[i] = gshfl(vq, i, G);
+        NOC_UNROLL for (int j = i; j < NX; ++j) S(i, j) = gb(sn[i], j);
+      NOC_UNROLL for (int i = 0; i < NX; ++i) v[i] = gb(vq, i);
       if (valid && a.S) gstore<NX>(a.S + ((tN + traj + s) * NX + q) * NX, sn);
       if (valid && a.v) a.v[(tN + traj + s) * NX + q] = vq;
       // stage s-1 has landed in the other buffer (and this stage's reads of `buf` are done
@@ -307,14 +341,14 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
     double uu = dv;
     NOC_UNROLL for (int k = 0; k < NX; ++k) uu += kr[k] * x[k];
     double u[NU];
-    NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = gshfl(uu, j, G);
+    NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = gb(uu, j);
     double xn = cv;
     NOC_UNROLL for (int k = 0; k < NX; ++k) xn += ar[k] * x[k];
     NOC_UNROLL for (int j = 0; j < NU; ++j) xn += br[j] * u[j];
     const size_t si = tN + s;
     if (valid && a.du && q < NU) a.du[si * NU + q] = uu;
     if (valid && a.dx) a.dx[(tN + traj + s + 1) * NX + q] = xn;
-    NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = gshfl(xn, i, G);
+    NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = gb(xn, i);
   }
 }
 
