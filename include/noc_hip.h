@@ -41,7 +41,13 @@ extern "C" {
 int noc_abi_version(void);
 const char* noc_last_error(void);
 int noc_kkt_supported(int nx, int nu);
+/* Lanes per trajectory used when a solve is called with lanes = 0 (batch-agnostic). */
 int noc_kkt_default_lanes(int nx, int nu, int N);
+/* Batch-aware choice for B trajectories on the current device (chunks of >= 3-4 stages per lane,
+ * then enough waves to fill every SIMD); what the Python host passes explicitly.  -1 on bad
+ * dimensions.  A caller that uses it passes the result as `lanes` to every call of the solve
+ * (including noc_kkt_gains_on_chip and the tiled-layout helpers). */
+int noc_kkt_pick_lanes(int nx, int nu, int N, int B);
 /* 1 if the fused solve (noc_kkt_solve / _tiled) with these sizes keeps the gains K, d in LDS
  * between its backward and forward phases, so K and d may be passed as NULL. */
 int noc_kkt_gains_on_chip(int nx, int nu, int N, int lanes);

@@ -66,6 +66,38 @@ int kkt_default_lanes(int nx, int nu, int N) {
   if (nx >= 8) return 1;
   return N >= 160 ? 32 : 64;
 }
+
+// SIMDs of the current device (4 per CU); 1024 (MI355X: 256 CUs) when no device is visible.
+static int device_simds() {
+  static int simds = 0;
+  if (simds == 0) {
+    int n = 0, dev = 0, cus = 0;
+    if (hipGetDeviceCount(&n) == hipSuccess && n > 0 && hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+      simds = 4 * cus;
+    else
+      simds = 1024;
+    (void)hipGetLastError();
+  }
+  return simds;
+}
+
+// Batch-aware lanes per trajectory (the measured lanes x horizon x batch sweep,
+// profiles/r01/session4/lanes_policy/): (1) the longest-parallel split whose chunks still hold
+// >= cmin stages (the cross-lane combine is amortised over the chunk: nx = 2 needs 3, nx = 4 four;
+// shorter chunks are combine-bound, longer ones serialise the lane and, at L = 32 and N >= 300,
+// the on-chip gains cap residency at 6 waves/CU), then (2) double L while the batch gives fewer
+// waves than the device has SIMDs (a half-empty chip loses more than a short chunk costs).
+int kkt_pick_lanes(int nx, int nu, int N, int B) {
+  if (nx >= 8) return kkt_default_lanes(nx, nu, N);
+  const int cmin = nx <= 2 ? 3 : 4;
+  int L = 8;
+  for (int c = 64; c >= 8; c /= 2)
+    if (N >= cmin * c) { L = c; break; }
+  const long simds = device_simds();
+  while (L < 64 && (long)B * L < 64 * simds) L *= 2;
+  return L;
+}
 }  // namespace noc
 
 extern "C" {
@@ -75,6 +107,10 @@ void noc_debug_set_ablation(int bits) { g_ablate = bits; }
 const char* noc_last_error(void) { return g_last_error.c_str(); }
 int noc_kkt_supported(int nx, int nu) { return noc::kkt_supported(nx, nu) ? 1 : 0; }
 int noc_kkt_default_lanes(int nx, int nu, int N) { return noc::kkt_default_lanes(nx, nu, N); }
+int noc_kkt_pick_lanes(int nx, int nu, int N, int B) {
+  if (check_dims(nx, nu, N, B, 0)) return -1;
+  return noc::kkt_pick_lanes(nx, nu, N, B);
+}
 int noc_kkt_gains_on_chip(int nx, int nu, int N, int lanes) {
   if (check_dims(nx, nu, N, 1, lanes)) return 0;
   const int L = lanes ? lanes : noc::kkt_default_lanes(nx, nu, N);

@@ -38,6 +38,7 @@ hipError_t kkt_dispatch_4x1(const KKTArgs& a, int lanes, hipStream_t stream);
 hipError_t kkt_dispatch_8x4(const KKTArgs& a, int lanes, hipStream_t stream);
 bool kkt_supported(int nx, int nu);
 int kkt_default_lanes(int nx, int nu, int N);
+int kkt_pick_lanes(int nx, int nu, int N, int B);
 
 hipError_t ipm_prepare(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                        hipStream_t s);

@@ -22,6 +22,7 @@ SIGNATURES = {
     "noc_last_error": (ctypes.c_char_p, []),
     "noc_kkt_supported": (_i, [_i, _i]),
     "noc_kkt_default_lanes": (_i, [_i, _i, _i]),
+    "noc_kkt_pick_lanes": (_i, [_i, _i, _i, _i]),
     "noc_kkt_gains_on_chip": (_i, [_i, _i, _i, _i]),
     "noc_debug_set_ablation": (None, [_i]),
     "noc_kkt_solve": (_i, [_i] * 5 + [_dp] * 13 + [_dp] * 8 + [_dp]),

@@ -49,7 +49,7 @@ class BatchedIPM:
                 raise _lib.NocError("persistent solve needs lanes = 64 and a supported family / "
                                     "horizon (noc_ipm_solve_supported)")
             lanes = 64
-        self.lanes = lanes or lib.noc_kkt_default_lanes(family.nx, family.nu, N)
+        self.lanes = lanes or lib.noc_kkt_pick_lanes(family.nx, family.nu, int(N), int(batch))
         if not lib.noc_family_supported(ctypes.byref(self.fam_c)):
             raise _lib.NocError(f"unsupported family kind={family.kind} nx={family.nx} nu={family.nu}")
         Bt, N, nx, nu = self.Bt, self.N, self.nx, self.nu

@@ -51,6 +51,13 @@ def _batched(*ts):
     return False, list(ts)
 
 
+def pick_lanes(nx: int, nu: int, N: int, B: int) -> int:
+    """Batch-aware lanes per trajectory for B trajectories (noc_kkt_pick_lanes)."""
+    L = _lib.load().noc_kkt_pick_lanes(nx, nu, N, B)
+    _lib.check(0 if L > 0 else L, "noc_kkt_pick_lanes")
+    return L
+
+
 def gains_on_chip(nx: int, nu: int, N: int, lanes: int = 0) -> bool:
     """True if the fused solve keeps K, d in LDS (noc_kkt_gains_on_chip), so they may be omitted."""
     return _lib.load().noc_kkt_gains_on_chip(nx, nu, N, lanes) == 1
@@ -74,6 +81,7 @@ def kkt_solve(A, B, Q, R, M, r, P, reg=None, x0=None, q=None, c=None, p=None, ac
     dev = A.device
     if active is not None:
         active = active.to(device=dev, dtype=torch.int32).contiguous()
+    lanes = lanes or pick_lanes(nx, nu, N, Bt)
     if out is None:
         f64 = dict(device=dev, dtype=torch.float64)
         gains = want_gains or not gains_on_chip(nx, nu, N, lanes)

@@ -43,6 +43,25 @@ def test_supported_shapes_and_lanes():
     assert lib.noc_kkt_default_lanes(4, 1, 200) in (8, 16, 32, 64)
 
 
+def test_batch_aware_lane_policy_picks_the_measured_best():
+    """noc_kkt_pick_lanes against the lanes sweep of profiles/r01/session4/lanes_policy/ (MI355X,
+    1024 SIMDs -- also the no-device default here): the fastest L of each measured (N, B), or one
+    within 4 % of it."""
+    from noc import _lib
+    lib = _lib.load()
+    cases = {  # (nx, nu, N, B): acceptable L (measured best first)
+        (4, 1, 50, 4096): (16, 8), (4, 1, 100, 4096): (16, 32), (4, 1, 150, 4096): (32,),
+        (4, 1, 200, 4096): (32,), (4, 1, 300, 4096): (64,), (4, 1, 400, 4096): (64,),
+        (4, 1, 200, 1024): (32, 64), (4, 1, 200, 16384): (32,),
+        (2, 1, 100, 1024): (64,), (2, 1, 100, 4096): (32, 16), (2, 1, 100, 16384): (32,),
+    }
+    for (nx, nu, N, B), ok in cases.items():
+        assert lib.noc_kkt_pick_lanes(nx, nu, N, B) in ok, (nx, nu, N, B)
+    assert lib.noc_kkt_pick_lanes(2, 1, 50, 1) == 64      # a lone trajectory takes the whole wave
+    assert lib.noc_kkt_pick_lanes(8, 4, 512, 16384) == 1  # nx = 8: the group solve
+    assert lib.noc_kkt_pick_lanes(3, 1, 50, 1) == -1      # unsupported shape
+
+
 def test_gains_on_chip_query_and_required_workspace():
     """K, d may be NULL only where the fused solve keeps them in LDS (20 KB per 64-lane block)."""
     from noc import _lib
