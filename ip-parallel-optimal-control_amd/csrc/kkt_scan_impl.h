@@ -37,6 +37,10 @@
 #define NOC_KKT_WAVES_PER_SIMD 2
 #endif
 
+#ifndef NOC_SCAN_NT
+#define NOC_SCAN_NT 1
+#endif
+
 namespace noc {
 
 template <int NX, int NU>
@@ -95,8 +99,14 @@ NOC_DEV void load_AB(const KKTArgs& a, int traj, size_t si, int j, int l, int cm
                      Mat<NX, NX>& A, Mat<NX, NU>& Bm, Vec<NX>& c) {
   set_zero(c);
   if constexpr (TILED) {
+#if NOC_SCAN_NT
+    // A, B are read for the last time here (phase 4 / the forward-mode map)
+    tload_last<NX * NX, L>(a.A, traj, j, l, cmax, A.v);
+    tload_last<NX * NU, L>(a.Bm, traj, j, l, cmax, Bm.v);
+#else
     tload<NX * NX, L>(a.A, traj, j, l, cmax, A.v);
     tload<NX * NU, L>(a.Bm, traj, j, l, cmax, Bm.v);
+#endif
     if constexpr (AFF) { if (a.c) tload<NX, L>(a.c, traj, j, l, cmax, c.v); }
   } else {
     gload<NX * NX>(a.A + si * (NX * NX), A.v);
@@ -731,7 +741,14 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       double2* dst2 = reinterpret_cast<double2*>(dst);
       for (int i = l; i < (N + 1) * H; i += L) {
         const int s = i / H, e = 2 * (i - s * H);
+#if NOC_SCAN_NT
+        noc_dbl2 v;
+        v.x = slot[s * KD + e];
+        v.y = slot[s * KD + e + 1];
+        __builtin_nontemporal_store(v, reinterpret_cast<noc_dbl2*>(dst2 + i));
+#else
         dst2[i] = make_double2(slot[s * KD + e], slot[s * KD + e + 1]);
+#endif
       }
     } else {
       for (int i = l; i < (N + 1) * NX; i += L) {

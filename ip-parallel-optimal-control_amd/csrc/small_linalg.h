@@ -122,6 +122,22 @@ NOC_DEV void tload(const double* __restrict__ base, int traj, int j, int l, int 
     NOC_UNROLL for (int e = 0; e < E; ++e) dst[e] = p[(size_t)e * L];
   }
 }
+// the same for a last use of the data: non-temporal loads (streaming cache policy), so the
+// blocks a later phase still re-reads keep the cache capacity
+typedef double noc_dbl2 __attribute__((ext_vector_type(2)));
+template <int E, int L>
+NOC_DEV void tload_last(const double* __restrict__ base, int traj, int j, int l, int cmax, double* dst) {
+  const double* p = base + tile_base<E, L>(traj, j, l, cmax);
+  if constexpr (E % 2 == 0) {
+    NOC_UNROLL for (int q = 0; q < E / 2; ++q) {
+      const noc_dbl2 v = __builtin_nontemporal_load(reinterpret_cast<const noc_dbl2*>(p + (size_t)q * 2 * L));
+      dst[2 * q] = v.x;
+      dst[2 * q + 1] = v.y;
+    }
+  } else {
+    NOC_UNROLL for (int e = 0; e < E; ++e) dst[e] = __builtin_nontemporal_load(p + (size_t)e * L);
+  }
+}
 template <int E, int L>
 NOC_DEV void tstore(double* __restrict__ base, int traj, int j, int l, int cmax, const double* src) {
   double* p = base + tile_base<E, L>(traj, j, l, cmax);
