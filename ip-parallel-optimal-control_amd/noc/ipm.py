@@ -49,7 +49,11 @@ class BatchedIPM:
                 raise _lib.NocError("persistent solve needs lanes = 64 and a supported family / "
                                     "horizon (noc_ipm_solve_supported)")
             lanes = 64
-        self.lanes = lanes or lib.noc_kkt_pick_lanes(family.nx, family.nu, int(N), int(batch))
+        # lanes = 0: the batch-agnostic default.  The batch-aware pick (noc_kkt_pick_lanes) is tuned for
+        # all-active launches; inside the loop the active set shrinks and wide segments win
+        # (cart-pole N=100 B=4096: 0.124 ms per device step at 64 lanes vs 0.136 at the pick's 16,
+        # profiles/r01/session4/ipm_lanes/)
+        self.lanes = lanes or lib.noc_kkt_default_lanes(family.nx, family.nu, N)
         if not lib.noc_family_supported(ctypes.byref(self.fam_c)):
             raise _lib.NocError(f"unsupported family kind={family.kind} nx={family.nx} nu={family.nu}")
         Bt, N, nx, nu = self.Bt, self.N, self.nx, self.nu

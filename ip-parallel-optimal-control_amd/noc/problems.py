@@ -189,8 +189,11 @@ def make_bench_blocks(name: str, N: int, batch: int, seed: int = 0, device="cuda
     (`tiled`: noc.lqt.TiledBlocks).  natural=True also returns the natural-layout copies
     (A, B, Q, R, M, r, P) for checks.  `reg`, `x`, `u` are natural."""
     from .ipm import BatchedIPM
+    from .lqt import pick_lanes
     ocp = make_problem(name, N)
     x0, u0 = initial_conditions(name, N, batch, seed)
+    # one all-active KKT launch over the batch: the batch-aware lanes policy
+    lanes = lanes or pick_lanes(ocp.family.nx, ocp.family.nu, N, batch)
     eng = BatchedIPM(ocp.family, N, batch, device=device, lanes=lanes)
     eng.load(u0, x0)
     eng.init(bp0=0.1)

@@ -70,6 +70,25 @@ def test_pendulum_par_solve_matches_oracle():
     assert np.max(np.abs(U - Ur)) < 1e-6
 
 
+@pytest.mark.parametrize("lanes", [8, 16, 32])
+def test_multilaunch_solve_at_every_scan_width_matches_oracle(lanes):
+    """The multi-launch device loop at the narrower scan widths the batch-aware lanes policy
+    (noc_kkt_pick_lanes) chooses for large batches: same counts and iterates as the oracle."""
+    from noc import problems
+    from noc.par_interior_point_newton import par_interior_point_optimal_control
+    from oracle import noc_oracle as O
+    N = 50
+    ocp = problems.pendulum(1.0 / N)
+    u0 = 0.1 * np.random.default_rng(1).normal(size=(N, 1))
+    x0 = np.array([0.1, -0.1])
+    U, it, info = par_interior_point_optimal_control(ocp, u0, x0, lanes=lanes, return_info=True)
+    prob = _oracle_problem("pendulum", N)
+    Ur, itr, solves_r = O.par_interior_point_optimal_control(prob, u0, x0, terminal="stage0")
+    assert it == itr == 70
+    assert info["kkt_solves"] == solves_r == 87
+    assert np.max(np.abs(U - Ur)) < 1e-6
+
+
 def test_pendulum_seq_solve_matches_oracle():
     from noc import problems
     from noc.seq_interior_point_newton import seq_interior_point_optimal_control

@@ -13,9 +13,10 @@ name = sys.argv[1] if len(sys.argv) > 1 else "cartpole"
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 B = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 persistent = (sys.argv[4] == "persistent") if len(sys.argv) > 4 else False
+lanes = int(sys.argv[5]) if len(sys.argv) > 5 else 0   # 0: the batch-aware policy
 ocp = problems.make_problem(name, N)
 x0, u0 = problems.initial_conditions(name, N, B, seed=11)
-eng = BatchedIPM(ocp.family, N, B, persistent=persistent)
+eng = BatchedIPM(ocp.family, N, B, persistent=persistent, lanes=lanes)
 eng.load(u0, x0)
 eng.solve(max_steps=16)   # warm-up (kernels loaded, caches)
 torch.cuda.synchronize()
