@@ -125,6 +125,8 @@ int noc_par_fwd_pass(int nx, int nu, int N, int B, int lanes,
 #define NOC_PHASE_SOLVE 2
 #define NOC_PHASE_DONE 3
 #define NOC_PHASE_ROLLED 4 /* rolled out, waiting to be promoted to LINEARIZE (two-stream loop) */
+#define NOC_PHASE_ROLLOUT_PENDING 5 /* a barrier stage ended in the last trial; noc_ipm_promote (or
+                                       the single-stream noc_ipm_step) starts its rollout */
 
 #define NOC_MODE_PAR 0 /* par_interior_point_newton semantics (retry loop, reg = rp*|cu|) */
 #define NOC_MODE_SEQ 1 /* seq_interior_point_newton semantics (one accept/reject, reg = mu) */
@@ -166,13 +168,17 @@ int noc_ipm_prepare(const noc_family* fam, const noc_ipm_ws* ws, int mode, int t
                     void* stream);
 /* trial point, gain ratio, regularisation update, accept, stop test, barrier schedule. */
 int noc_ipm_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* stream);
-/* one device iteration: prepare + noc_kkt_solve(active = phase SOLVE) + trial. */
+/* one device iteration: prepare + noc_kkt_solve(active = phase SOLVE) + trial.  lanes must be 0
+ * or ws->lanes (the workspace's tiled layout fixes it); anything else is rejected. */
 int noc_ipm_step(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, int lanes,
                  void* stream);
 /* Two-stream form of one iteration (rollouts overlap the other trajectories' Newton step):
  *   roll stream : wait(prev main event); noc_ipm_rollout      (ROLLOUT -> ROLLED)
  *   main stream : noc_ipm_step_main (LINEARIZE..SOLVE..trial); wait(roll event);
  *                 noc_ipm_promote                              (ROLLED  -> LINEARIZE)
+ * The trial marks a trajectory whose barrier stage ended NOC_PHASE_ROLLOUT_PENDING; only promote
+ * (after the main stream waited on the roll event) turns that into ROLLOUT, so a rollout never
+ * runs concurrently with the trial that writes its controls.
  * Every trajectory still performs exactly its own reference sequence of operations. */
 int noc_ipm_rollout(const noc_family* fam, const noc_ipm_ws* ws, void* stream);
 int noc_ipm_step_main(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal,

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
               NOC_UNROLL for (int j = 0; j < NX; ++j) KK[((size_t)t * NU + i) * NX + j] = -Y[i][1 + j];
             }
             pred += -0.5 * Qu[i] * Y[i][0];
-            hn = fmax(hn, fabs(Qu[i]));  // Hu = Qu (D:56, D:120)
+            hn = nan_max(hn, fabs(Qu[i]));  // Hu = Qu (D:56, D:120)
           }
           // Vx = Qx - Qu'Quu^-1 Qux, Vxx = Qxx - Qxu Quu^-1 Qux (D:54-55)
           NOC_UNROLL for (int j = 0; j < NX; ++j) {

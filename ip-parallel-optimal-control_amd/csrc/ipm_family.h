@@ -133,6 +133,10 @@ NOC_DEV double readlane_d(double v, int lane) {  // wave-uniform broadcast of on
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// max that propagates NaN like jnp.max (fmax drops it): a NaN |Hu| must fail the < 1e-4 stop
+// test exactly as in the reference (P:158, P:199; D:120)
+NOC_DEV double nan_max(double a, double b) { return (a != a || b != b) ? NAN : fmax(a, b); }
+
 NOC_DEV double wave_sum(double v) {
   NOC_UNROLL for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;

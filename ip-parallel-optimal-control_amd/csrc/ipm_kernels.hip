@@ -26,11 +26,18 @@ namespace noc {
 // is inherently sequential; every lane evaluates it redundantly (free in SIMD) with u_k broadcast
 // from registers (v_readlane), so the dependent chain never waits on memory: controls are read and
 // states written 64 stages at a time, coalesced.
+// take_pending: also roll out trajectories the last trial marked ROLLOUT_PENDING (the
+// single-stream loop, where nothing else runs concurrently).  The two-stream loop passes 0: its
+// rollout runs beside the main stream's trial kernel, which may mark a trajectory (after writing
+// its new u) at any moment; only the main stream's promote, ordered after that trial, turns the
+// mark into ROLLOUT, so this kernel sees exactly the trajectories marked before it was launched.
 template <int KIND, int NX, int NU>
-__global__ __launch_bounds__(256) void rollout_kernel(noc_family prm, noc_ipm_ws w) {
+__global__ __launch_bounds__(256) void rollout_kernel(noc_family prm, noc_ipm_ws w, int take_pending) {
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (b >= w.Bt || w.phase[b] != NOC_PHASE_ROLLOUT) return;  // uniform per wave
+  if (b >= w.Bt) return;
+  const int ph = w.phase[b];
+  if (!(ph == NOC_PHASE_ROLLOUT || (take_pending && ph == NOC_PHASE_ROLLOUT_PENDING))) return;  // uniform per wave
   Fam<KIND, NX, NU> f(prm);
   const int N = w.N;
   double x[NX];
@@ -59,9 +66,13 @@ __global__ __launch_bounds__(256) void rollout_kernel(noc_family prm, noc_ipm_ws
   if (lane == 0) w.phase[b] = NOC_PHASE_ROLLED;
 }
 
+// ROLLED -> LINEARIZE; ROLLOUT_PENDING -> ROLLOUT (the next step's rollout picks it up)
 __global__ __launch_bounds__(256) void promote_kernel(noc_ipm_ws w) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < w.Bt && w.phase[b] == NOC_PHASE_ROLLED) w.phase[b] = NOC_PHASE_LINEARIZE;
+  if (b >= w.Bt) return;
+  const int ph = w.phase[b];
+  if (ph == NOC_PHASE_ROLLED) w.phase[b] = NOC_PHASE_LINEARIZE;
+  else if (ph == NOC_PHASE_ROLLOUT_PENDING) w.phase[b] = NOC_PHASE_ROLLOUT;
 }
 
 // thread per (trajectory, chunk slot, lane) in tiled order: the A/B stores are coalesced
@@ -186,7 +197,7 @@ __global__ __launch_bounds__(64) void costate_scan_kernel(noc_family prm, noc_ip
       double r = cu[jj];
       NOC_UNROLL for (int i = 0; i < NX; ++i) r += Bm[i * NU + jj] * lam[i];
       rr[jj] = r;
-      hu = fmax(hu, fabs(r));
+      hu = nan_max(hu, fabs(r));
       g2s += cu[jj] * cu[jj];
     }
     tstore_rt<NU>(w.r, L, ch.cmax, b, k - start, l, rr);
@@ -206,7 +217,7 @@ __global__ __launch_bounds__(64) void costate_scan_kernel(noc_family prm, noc_ip
   NOC_UNROLL for (int off = L / 2; off > 0; off >>= 1) {
     cost += __shfl_xor(cost, off, L);
     g2s += __shfl_xor(g2s, off, L);
-    hu = fmax(hu, __shfl_xor(hu, off, L));
+    hu = nan_max(hu, __shfl_xor(hu, off, L));
   }
   if (l != 0) return;
   double P[NX * NX];
@@ -356,7 +367,9 @@ __global__ __launch_bounds__(256) void trial_kernel(noc_family prm, noc_ipm_ws w
     it = 0;
     rp = 1.0;                                             // P:134 / S:110
     rinc = 2.0;                                           // P:135 / S:111
-    phase = (nbp > 1e-4) ? NOC_PHASE_ROLLOUT : NOC_PHASE_DONE;  // P:243-245
+    // P:243-245; the rollout of the new stage happens in the next step (ROLLOUT_PENDING, see
+    // rollout_kernel)
+    phase = (nbp > 1e-4) ? NOC_PHASE_ROLLOUT_PENDING : NOC_PHASE_DONE;
   } else if (mode == NOC_MODE_PAR) {
     phase = end_iter ? NOC_PHASE_LINEARIZE : NOC_PHASE_SOLVE;
   } else {
@@ -388,8 +401,10 @@ __global__ __launch_bounds__(256) void init_kernel(noc_ipm_ws w, double bp0) {
 
 // ------------------------------------------------------------------------------------------------
 template <int KIND, int NX, int NU>
-static hipError_t rollout_t(const noc_family& p, const noc_ipm_ws& w, hipStream_t s) {
-  hipLaunchKernelGGL((rollout_kernel<KIND, NX, NU>), dim3((w.Bt + 3) / 4), dim3(256), 0, s, p, w);
+static hipError_t rollout_t(const noc_family& p, const noc_ipm_ws& w, hipStream_t s,
+                           int take_pending) {
+  hipLaunchKernelGGL((rollout_kernel<KIND, NX, NU>), dim3((w.Bt + 3) / 4), dim3(256), 0, s, p, w,
+                     take_pending);
   return hipGetLastError();
 }
 
@@ -410,7 +425,7 @@ static hipError_t prepare_main_t(const noc_family& p, const noc_ipm_ws& w, int m
 template <int KIND, int NX, int NU>
 static hipError_t prepare_t(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                             hipStream_t s) {
-  hipError_t e = rollout_t<KIND, NX, NU>(p, w, s);
+  hipError_t e = rollout_t<KIND, NX, NU>(p, w, s, 1);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(promote_kernel, dim3((w.Bt + 255) / 256), dim3(256), 0, s, w);
   return prepare_main_t<KIND, NX, NU>(p, w, mode, terminal, s);
@@ -444,14 +459,14 @@ hipError_t ipm_prepare(const noc_family& p, const noc_ipm_ws& w, int mode, int t
 hipError_t ipm_rollout(const noc_family& p, const noc_ipm_ws& w, hipStream_t s) {
   switch (p.kind) {
     case NOC_FAMILY_PENDULUM:
-      if (p.nx == 2 && p.nu == 1) return rollout_t<NOC_FAMILY_PENDULUM, 2, 1>(p, w, s);
+      if (p.nx == 2 && p.nu == 1) return rollout_t<NOC_FAMILY_PENDULUM, 2, 1>(p, w, s, 0);
       break;
     case NOC_FAMILY_CARTPOLE:
-      if (p.nx == 4 && p.nu == 1) return rollout_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, w, s);
+      if (p.nx == 4 && p.nu == 1) return rollout_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, w, s, 0);
       break;
     case NOC_FAMILY_LINEAR:
-      if (p.nx == 2 && p.nu == 1) return rollout_t<NOC_FAMILY_LINEAR, 2, 1>(p, w, s);
-      if (p.nx == 8 && p.nu == 4) return rollout_t<NOC_FAMILY_LINEAR, 8, 4>(p, w, s);
+      if (p.nx == 2 && p.nu == 1) return rollout_t<NOC_FAMILY_LINEAR, 2, 1>(p, w, s, 0);
+      if (p.nx == 8 && p.nu == 4) return rollout_t<NOC_FAMILY_LINEAR, 8, 4>(p, w, s, 0);
       break;
     default: break;
   }

@@ -268,7 +268,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
             double r = in.cu[jj];
             NOC_UNROLL for (int i = 0; i < NX; ++i) r += in.Bm[i * NU + jj] * lam[i];
             o.rr[jj] = r;
-            hmax = valid ? fmax(hmax, fabs(r)) : hmax;
+            hmax = valid ? nan_max(hmax, fabs(r)) : hmax;
             g2s = valid ? g2s + in.cu[jj] * in.cu[jj] : g2s;
           }
           NOC_UNROLL for (int i = 0; i < NX; ++i) {
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         NOC_UNROLL for (int off = PL / 2; off > 0; off >>= 1) {
           csum += __shfl_xor(csum, off, PL);
           g2s += __shfl_xor(g2s, off, PL);
-          hmax = fmax(hmax, __shfl_xor(hmax, off, PL));
+          hmax = nan_max(hmax, __shfl_xor(hmax, off, PL));
         }
         if (terminal == NOC_TERMINAL_FINAL_COST && last) {  // hessian(final_cost) (S:66)
           double P[NX * NX];

@@ -18,11 +18,12 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
-bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-
-int check_ptr(const void* p, const char* name, bool required) {
+// align: 16 where the kernels read / write the array with 16-byte vector accesses (the fp64 KKT
+// fields), the natural alignment (8 for fp64, 4 for int32) elsewhere
+int check_ptr(const void* p, const char* name, bool required, unsigned align = 16) {
   if (!p) return required ? fail(-2, std::string("required pointer is NULL: ") + name) : 0;
-  if (!aligned16(p)) return fail(-3, std::string("pointer not 16-byte aligned: ") + name);
+  if (reinterpret_cast<uintptr_t>(p) & (align - 1))
+    return fail(-3, std::string("pointer not ") + std::to_string(align) + "-byte aligned: " + name);
   return 0;
 }
 
@@ -144,7 +145,10 @@ static int kkt_common(int mode, int tiled, int nx, int nu, int N, int B, int lan
   if ((rc = check_ptr(v, "v", false))) return rc;
   if ((rc = check_ptr(dx, "dx", false))) return rc;
   if ((rc = check_ptr(du, "du", false))) return rc;
-  if (reg && (reinterpret_cast<uintptr_t>(reg) & 7u)) return fail(-3, "reg not 8-byte aligned");
+  if ((rc = check_ptr(reg, "reg", false, 8))) return rc;
+  if ((rc = check_ptr(pred, "pred", false, 8))) return rc;
+  if ((rc = check_ptr(feasible, "feasible", false, 4))) return rc;
+  if ((rc = check_ptr(active, "active", false, 4))) return rc;
   if (B == 0) return 0;
   noc::KKTArgs a{};
   a.N = N;
@@ -283,7 +287,10 @@ static int kkt_and_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, 
 
 int noc_ipm_step(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, int lanes,
                  void* stream) {
-  (void)lanes;
+  // lanes: 0 = the workspace's; any other value must equal it (the blocks are laid out for it)
+  if (ws && lanes != 0 && lanes != ws->lanes)
+    return fail(-1, "noc_ipm_step: lanes (" + std::to_string(lanes) + ") differs from the workspace's (" +
+                        std::to_string(ws->lanes) + "); pass 0 or ws->lanes");
   int rc = noc_ipm_prepare(fam, ws, mode, terminal, stream);
   if (rc) return rc;
   return kkt_and_trial(fam, ws, mode, stream);
@@ -366,9 +373,9 @@ int noc_ddp_solve(const noc_family* fam, int N, int Bt, const double* x0, double
   if (!(bp0 > 0.0)) return fail(-1, "bp0 must be > 0");
   if (max_passes < 1) return fail(-1, "max_passes must be >= 1");
   int rc = 0;
-  if ((rc = check_ptr(x0, "x0", true)) || (rc = check_ptr(u, "u", true)) ||
-      (rc = check_ptr(work, "work", true)) || (rc = check_ptr(iterations, "iterations", true)) ||
-      (rc = check_ptr(passes, "passes", true)) || (rc = check_ptr(done, "done", true)))
+  if ((rc = check_ptr(x0, "x0", true, 8)) || (rc = check_ptr(u, "u", true, 8)) ||
+      (rc = check_ptr(work, "work", true, 8)) || (rc = check_ptr(iterations, "iterations", true, 4)) ||
+      (rc = check_ptr(passes, "passes", true, 4)) || (rc = check_ptr(done, "done", true, 4)))
     return rc;
   if (Bt == 0) return 0;
   return hip_status(noc::ddp_solve(*fam, N, Bt, x0, u, work, iterations, passes, done, bp0,

@@ -36,6 +36,7 @@ SIGNATURES = {
 # --- structs of include/noc_hip.h --------------------------------------------------------------
 FAMILY_PENDULUM, FAMILY_CARTPOLE, FAMILY_LINEAR = 1, 2, 3
 PHASE_ROLLOUT, PHASE_LINEARIZE, PHASE_SOLVE, PHASE_DONE, PHASE_ROLLED = 0, 1, 2, 3, 4
+PHASE_ROLLOUT_PENDING = 5
 MODE_PAR, MODE_SEQ = 0, 1
 TERMINAL_FINAL_COST, TERMINAL_STAGE0 = 0, 1
 

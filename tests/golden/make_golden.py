@@ -67,10 +67,57 @@ def ipm_fixtures():
     return out
 
 
+def newton_block_fixtures():
+    """golden_v2: the LQ blocks of a real first Newton step (bp = 0.1, rp = 1, so
+    reg = ||cu||_F, P:116-118) of the BASELINE problems -- pendulum N=100 (c2) and cart-pole
+    N=200 (c3), two trajectories each from the SURVEY §8d input distributions -- linearised by
+    the autodiff oracle (P:13-42), and the KKT step of each computed by the FAITHFUL sequential
+    Riccati (S:42-90: Vxx propagated unsymmetrised, inv(Quu), eigh test), checked against the
+    dense KKT solve at generation time.  The GPU tests compare the HIP path with these committed
+    vectors directly (no live oracle)."""
+    out = {}
+    cases = [("pend100", PR.pendulum_ocp(1.0 / 100), 100, "pendulum"),
+             ("cart200", PR.cartpole_ocp(1.0 / 200), 200, "cartpole")]
+    for tag, tocp, N, name in cases:
+        prob = O.NumpyProblem(tocp)
+        rng = np.random.default_rng(2024 + N)
+        if name == "pendulum":
+            x0s = np.array([0.1, -0.1]) + 0.01 * rng.normal(size=(2, 2))
+        else:
+            x0s = np.array([0.01, 2 * np.pi - 0.01, 0.01, -0.01]) + 0.01 * rng.normal(size=(2, 4))
+        u0s = 0.1 * rng.normal(size=(2, N, 1))
+        blocks = {k: [] for k in ("x", "A", "B", "Q", "R", "M", "r", "P", "reg", "dx", "du", "pred",
+                                  "feasible", "K", "d")}
+        for b in range(2):
+            X = O.rollout(prob.dynamics, u0s[b], x0s[b])
+            L = O.linearize(prob, X, u0s[b], 0.1)
+            reg = float(np.linalg.norm(L["cu"]))
+            dx, du, pred, feas, K, d, S, v = O.kkt_solve(L["A"], L["B"], L["Q"], L["R"], L["M"],
+                                                         L["r"], L["P"], reg, symmetrize=False)
+            ddx, ddu, _ = O.dense_kkt(L["A"], L["B"], L["Q"], L["R"], L["M"], L["r"], L["P"], reg)
+            assert np.max(np.abs(ddx - dx)) < 1e-10 * max(1, np.abs(ddx).max())
+            assert np.max(np.abs(ddu - du)) < 1e-10 * max(1, np.abs(ddu).max())
+            for k, val in (("x", X), ("reg", reg), ("dx", dx), ("du", du), ("pred", pred),
+                           ("feasible", feas), ("K", K), ("d", d)):
+                blocks[k].append(np.asarray(val))
+            for k in ("A", "B", "Q", "R", "M", "r", "P"):
+                blocks[k].append(L[k])
+        out[f"{tag}/u0"] = u0s
+        out[f"{tag}/x0"] = x0s
+        for k, vals in blocks.items():
+            out[f"{tag}/{k}"] = np.stack(vals)
+    return out
+
+
 if __name__ == "__main__":
     data = {}
     data.update(lq_fixtures())
     data.update(ipm_fixtures())
     path = os.path.join(HERE, "golden_v1.npz")
-    np.savez_compressed(path, **data)
-    print("wrote", path, os.path.getsize(path), "bytes,", len(data), "arrays")
+    if "--v2-only" not in sys.argv:
+        np.savez_compressed(path, **data)
+        print("wrote", path, os.path.getsize(path), "bytes,", len(data), "arrays")
+    data2 = newton_block_fixtures()
+    path2 = os.path.join(HERE, "golden_v2.npz")
+    np.savez_compressed(path2, **data2)
+    print("wrote", path2, os.path.getsize(path2), "bytes,", len(data2), "arrays")

@@ -189,3 +189,25 @@ def test_ddp_queries_and_argument_errors_without_gpu():
     lin8 = problems.double_integrators(4, 0.001).family.to_c()
     assert lib.noc_ddp_solve(ctypes.byref(lin8), 10, 1, *args, 0.1, 10, None) < 0
     assert b"nx <= 4" in lib.noc_last_error()
+
+
+def test_alignment_checks_use_natural_alignment_for_scalars_and_flags():
+    """16-byte alignment is required only for the fp64 fields the kernels access with 16-byte
+    vector loads / stores; reg and pred need 8, feasible / active / DDP counters 4.
+    B = 0 validates and returns without a launch."""
+    from noc import _lib, problems
+    lib = _lib.load()
+    blocks = [16] * 6  # A, B, Q, R, M, r (fake, never dereferenced)
+
+    def solve(reg=16, pred=16, feasible=16, active=None, A=16):
+        return lib.noc_kkt_solve(4, 1, 10, 0, 32, A, *blocks[1:], None, None, 16, None, None, reg,
+                                 active, 16, 16, pred, feasible, 16, 16, None, None, None)
+    assert solve() == 0
+    assert solve(reg=24, pred=40, feasible=20, active=36) == 0   # natural alignment suffices
+    assert solve(reg=20) < 0 and b"reg" in lib.noc_last_error()
+    assert solve(feasible=18) < 0 and b"feasible" in lib.noc_last_error()
+    assert solve(A=24) < 0 and b"16-byte" in lib.noc_last_error()
+    pend = problems.pendulum(0.02).family.to_c()
+    # x0 / u / work at 8-byte offsets and int32 counters at 4-byte offsets: accepted (empty batch)
+    assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 0, 24, 40, 56, 20, 36, 52, 0.1, 10, None) == 0
+    assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 0, 20, 40, 56, 20, 36, 52, 0.1, 10, None) < 0

@@ -267,3 +267,39 @@ def test_solver_reproduces_survey_restatement_numbers(name, N, par_its, par_solv
     assert abs(c - cost) <= 1e-6 * abs(cost)
     Us, its = seq_interior_point_optimal_control(ocp, u0, x0)
     assert its == seq_its
+
+
+@pytest.mark.parametrize("name,N,Bt,lanes", [("pendulum", 60, 24, 64), ("cartpole", 100, 40, 32)])
+def test_two_stream_overlap_equals_single_stream_loop(name, N, Bt, lanes):
+    """The two-stream loop (rollouts on a second stream beside the Newton step, the default once
+    Bt*N >= 256k) forced on at a small size: a trajectory whose barrier stage ends is marked
+    ROLLOUT_PENDING by the trial and only promoted to ROLLOUT after the main stream waited on the
+    roll event, so it must give the same counters and bit-identical iterates as the single-stream
+    loop (the rollout could otherwise read controls the trial is still writing)."""
+    from noc import problems, _lib
+    from noc.ipm import BatchedIPM
+    ocp = problems.make_problem(name, N)
+    x0, u0 = problems.initial_conditions(name, N, Bt, seed=33)
+    res = []
+    for overlap in (True, False):
+        eng = BatchedIPM(ocp.family, N, Bt, lanes=lanes, overlap=overlap)
+        eng.load(u0, x0)
+        eng.solve(poll_every=4)
+        torch.cuda.synchronize()
+        res.append([t.cpu().numpy() for t in eng.result()] + [eng.t["phase"].cpu().numpy()])
+    (Uo, ito, so, pho), (Us, its, ss, phs) = res
+    assert np.all(pho == _lib.PHASE_DONE) and np.all(phs == _lib.PHASE_DONE)
+    assert np.array_equal(ito, its) and np.array_equal(so, ss)
+    assert np.array_equal(Uo, Us)
+
+
+def test_ipm_step_rejects_mismatched_lanes():
+    import ctypes
+    from noc import problems, _lib
+    from noc.ipm import BatchedIPM
+    ocp = problems.pendulum(1.0 / 20)
+    eng = BatchedIPM(ocp.family, 20, 2, lanes=64)
+    lib = _lib.load()
+    rc = lib.noc_ipm_step(ctypes.byref(eng.fam_c), ctypes.byref(eng.ws), _lib.MODE_PAR,
+                          _lib.TERMINAL_STAGE0, 32, _lib.stream_handle())
+    assert rc != 0 and b"lanes" in lib.noc_last_error()

@@ -281,11 +281,14 @@ def test_group_solve_linear8_blocks_properties():
     assert bool(torch.all(res.feasible == 1))
 
 
-@pytest.mark.parametrize("name,N,B,lanes", [("linear8", 512, 16384, 1), ("cartpole", 200, 65536, 32)])
+@pytest.mark.parametrize("name,N,B,lanes", [("linear8", 512, 16384, 1), ("cartpole", 200, 65536, 32),
+                                           ("pendulum", 100, 1024, 0), ("cartpole", 200, 4096, 0)])
 def test_full_size_bench_blocks_properties(name, N, B, lanes):
     """The bench path at BASELINE full sizes where the oracle cannot run on every trajectory:
-    c4 (linear8, N=512, B=16384, group solve on the grouped layout) and c5's global batch on ONE
-    GPU (cart-pole, N=200, B=65536 = 8 x 8192: 64-bit indexing of the tiled layout).  Properties:
+    c2 (pendulum, N=100, B=1024: the batch-aware pick = 64 lanes, register-cached chunks), c3
+    (cart-pole, N=200, B=4096: 32 lanes), c4 (linear8, N=512, B=16384, group solve on the grouped
+    layout) and c5's global batch on ONE GPU (cart-pole, N=200, B=65536 = 8 x 8192: 64-bit
+    indexing of the tiled layout).  Properties:
     dx_{k+1} = A dx_k + B du_k on every trajectory, all feasible, finite pred, and oracle parity
     on a strided sample of 8 trajectories including the last one."""
     from noc import lqt

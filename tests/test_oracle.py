@@ -166,3 +166,27 @@ def test_golden_fixtures_reproduced():
     L = O.linearize(prob, gold["cart20/x"], gold["cart20/u"], 0.1)
     for k in ("A", "B", "Q", "R", "M", "r", "P"):
         assert _maxrel(L[k], gold[f"cart20/{k}"]) < 1e-12, k
+
+
+def test_golden_v2_newton_blocks_reproduced():
+    """golden_v2 (real c2 / c3 Newton blocks, faithful S:42-90 steps): the oracle regenerates the
+    committed blocks and steps, and the faithful and symmetrised Riccati agree on them to 1e-12
+    (so the GPU's symmetric-S scan is held to the faithful reference at 1e-10)."""
+    import os
+    from oracle import noc_oracle as O, problems as PR
+    gold = np.load(os.path.join(os.path.dirname(GOLDEN), "golden_v2.npz"))
+    for tag, tocp in (("pend100", PR.pendulum_ocp(1.0 / 100)), ("cart200", PR.cartpole_ocp(1.0 / 200))):
+        prob = O.NumpyProblem(tocp)
+        g = lambda k: gold[f"{tag}/{k}"]
+        for b in range(2):
+            X = O.rollout(prob.dynamics, g("u0")[b], g("x0")[b])
+            assert _maxrel(X, g("x")[b]) < 1e-13
+            L = O.linearize(prob, X, g("u0")[b], 0.1)
+            for k in ("A", "B", "Q", "R", "M", "r", "P"):
+                assert _maxrel(L[k], g(k)[b]) < 1e-12, (tag, k)
+            blocks = [g(k)[b] for k in ("A", "B", "Q", "R", "M", "r", "P")]
+            dx, du, pred, feas, K, d, _, _ = O.kkt_solve(*blocks, g("reg")[b], symmetrize=False)
+            for k, v in (("dx", dx), ("du", du), ("pred", pred), ("K", K), ("d", d)):
+                assert _maxrel(v, g(k)[b]) < 1e-12, (tag, k)
+            sdx, sdu = O.kkt_solve(*blocks, g("reg")[b], symmetrize=True)[:2]
+            assert _maxrel(sdx, dx) < 1e-12 and _maxrel(sdu, du) < 1e-12
