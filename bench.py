@@ -2,16 +2,21 @@
 """Benchmark: batched KKT Newton-steps/sec of the parallel-in-time IPM hot path on MI355X.
 
 Metric (BASELINE.json): "KKT Newton-steps/sec at (horizon N x batch)".  One step = one batched
-KKT solve (paroc.par_bwd_pass + par_fwd_pass replacement, noc_kkt_solve) of `batch` cart-pole
-trajectories with horizon N = 200 (BASELINE config c3), the LQ blocks being the real first
-Newton iterate (bp = 0.1) produced on the device by the linearisation kernels, resident in HBM
-before timing.  value = trajectories x steps / second, summed over ranks (weak scaling: every
-rank owns `batch` trajectories; no collective on the data path, one all-reduce(max) of the
-timing).  Roofline: algorithmic bytes per launch / measured launch time vs the
-8 TB/s HBM peak.  cpu_baseline: the plain-C restatement of the reference's sequential Riccati
-(oracle/kkt_ref.c, OpenMP) on a bounded sample of the same blocks, rank 0, N=1 only.
+KKT solve (paroc.par_bwd_pass + par_fwd_pass replacement, noc_kkt_solve) of cart-pole
+trajectories with horizon N = 200, the LQ blocks being the real first Newton iterate (bp = 0.1)
+produced on the device by the linearisation kernels, resident in HBM before timing.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Scaling (north_star: "cartpole N=200 batch=4096 at 1, 2, 4 and 8 GPUs"): by default the GLOBAL
+batch of 4096 trajectories (BASELINE config c3) is split over the ranks with
+noc.distributed.shard_bounds (strong scaling; at --gpus 1 this is c3 itself).  --batch B instead
+gives every rank B trajectories (weak scaling; c5 = --batch 8192 on 8 GPUs).  No collective on the
+data path; one all-reduce(max) of the timing.  value = global trajectories x steps / the slowest
+rank's time.  Roofline: the slowest rank's algorithmic bytes per launch / its
+launch time vs the 8 TB/s HBM peak.  cpu_baseline: the plain-C restatement of the reference's
+sequential Riccati (oracle/kkt_ref.c, OpenMP) on a bounded sample of the same blocks, rank 0,
+N=1 only.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch G | --batch B]
        (multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
 """
 import argparse
@@ -24,10 +29,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ip-parallel-optimal-control_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-CONFIG_LABEL = {("cartpole", 200, 4096): "BASELINE c3 per GPU; weak scaling over --gpus (c5's 65536 = --batch 8192 on 8 GPUs)",
+CONFIG_LABEL = {("cartpole", 200, 4096): "BASELINE c3",
                 ("pendulum", 100, 1024): "BASELINE c2",
                 ("linear8", 512, 16384): "BASELINE c4",
-                ("cartpole", 200, 8192): "BASELINE c5 per-GPU shard (65536 / 8)"}
+                ("cartpole", 200, 65536): "BASELINE c5 (8192 per GPU on 8 GPUs)"}
 
 
 def algorithmic_bytes(nx, nu, N, B):
@@ -95,11 +100,24 @@ def residual_vs_seq_ref(out, ref, sample):
     return res
 
 
-def ipm_solve_rate(problem, N, B, rank):
-    """End-to-end: the whole interior-point solve (P:228-254) of the same B trajectories with the
-    persistent kernel (noc_ipm_solve, one launch), timed with HIP events.  Reported beside the KKT
-    metric: trajectories x Newton KKT solves actually performed / wall time."""
+def allreduce(vals, op="sum"):
+    """All-reduce of a few fp64 scalars over the bench's process group (RCCL on the GPUs; the
+    gloo rehearsal mode reduces on the host)."""
     import torch
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    return t.tolist()
+
+
+def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
+    """End-to-end: the whole interior-point solve (P:228-254) of this rank's B trajectories with
+    the persistent kernel (noc_ipm_solve, one launch), timed with HIP events; over ranks the wall
+    time is the max and the solve counts are summed.  Reported beside the KKT metric:
+    trajectories x Newton KKT solves actually performed / wall time."""
+    import torch
+    import torch.distributed as dist
     from noc import problems
     from noc.ipm import BatchedIPM, persistent_supported
     ocp = problems.make_problem(problem, N)
@@ -108,12 +126,14 @@ def ipm_solve_rate(problem, N, B, rank):
         # interior-point loop), so its KKT line is already the end-to-end step
         return {"skipped": "no persistent instance for this family / horizon (c4 is LQ-only in "
                            "the reference: one KKT solve per MPC step, LM:67-84)"}
-    x0, u0 = problems.initial_conditions(problem, N, B, seed=11 + rank)
+    x0, u0 = problems.initial_conditions(problem, N, B, seed=seed_base + rank)
     eng = BatchedIPM(ocp.family, N, B, persistent=True)
     eng.load(u0, x0)
     eng.solve(max_steps=8)  # warm-up
     eng.load(u0, x0)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     eng.solve()
@@ -122,11 +142,17 @@ def ipm_solve_rate(problem, N, B, rank):
     ms = ev0.elapsed_time(ev1)
     U, its, solves = (t.cpu() for t in eng.result())
     done = int((eng.t["phase"] == 3).sum().item())
-    return {"what": "whole barrier schedule, noc_ipm_solve (one wave per trajectory, one launch)",
-            "trajectories": B, "wall_ms": ms, "kkt_solves": int(solves.sum()),
-            "kkt_solves_per_s": float(solves.sum()) / (ms * 1e-3),
-            "mean_newton_iters": float(its.double().mean()), "max_kkt_solves": int(solves.max()),
-            "converged": done}
+    tot = [float(solves.sum()), float(done), float(its.double().sum()), float(B)]
+    mx = [ms, float(solves.max())]
+    if world > 1:
+        tot = allreduce(tot, "sum")
+        mx = allreduce(mx, "max")
+    return {"what": "whole barrier schedule, noc_ipm_solve (one wave per trajectory, one launch "
+                    "per rank)",
+            "trajectories": int(tot[3]), "wall_ms": mx[0], "kkt_solves": int(tot[0]),
+            "kkt_solves_per_s": tot[0] / (mx[0] * 1e-3),
+            "mean_newton_iters": tot[2] / max(tot[3], 1.0), "max_kkt_solves": int(mx[1]),
+            "converged": int(tot[1])}
 
 
 def main():
@@ -136,7 +162,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--problem", default="cartpole")
     ap.add_argument("--horizon", type=int, default=200)
-    ap.add_argument("--batch", type=int, default=4096, help="trajectories per GPU")
+    ap.add_argument("--global-batch", type=int, default=4096,
+                    help="total trajectories, split over the ranks (strong scaling; default c3)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="trajectories per GPU instead (weak scaling)")
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--layout", choices=["tiled", "natural"], default="tiled",
                     help="HBM layout of the LQ blocks (tiled = what the linearisation kernels write)")
@@ -152,12 +181,26 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # NOC_BENCH_REHEARSAL=1: every rank on cuda:0 over gloo -- rehearses the N > 1 code path on a
+    # one-GPU box (timings then share one GPU and mean nothing)
+    rehearsal = os.environ.get("NOC_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from noc import lqt, problems, _lib
 
-    N, B = args.horizon, args.batch
+    N = args.horizon
+    if args.batch is not None:        # weak scaling: every rank owns --batch trajectories
+        B, G, scaling = args.batch, args.batch * world, "weak"
+    else:                             # strong scaling: the global batch is sharded
+        from noc.distributed import shard_bounds
+        lo, hi = shard_bounds(args.global_batch, world, rank)
+        B, G, scaling = hi - lo, args.global_batch, "strong"
     # lanes 8..64: the parallel-in-time scan on the lane-interleaved layout; lanes 1: the
     # horizon-sequential group solve on the grouped layout (the nx = 8 default).  Either way the
     # blocks are what the device linearisation writes for that solver.
@@ -197,12 +240,12 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / args.steps          # HIP-event time per launch (stream)
     ms = wall * 1e3 / args.steps
     if world > 1:
-        t = torch.tensor([ms, kern_ms], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms, kern_ms = float(t[0]), float(t[1])
+        ms, kern_ms = allreduce([ms, kern_ms], "max")
     feasible_frac = float(out.feasible.float().mean())
-    value = world * B * args.steps / (ms * args.steps / 1e3)
+    value = G * args.steps / (ms * args.steps / 1e3)
     abytes = algorithmic_bytes(nx, nu, N, B)
+    if world > 1:  # the slowest rank's bytes (shards differ by at most one trajectory)
+        abytes = int(allreduce([abytes], "max")[0])
     achieved = abytes / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic(args.pmc_json, f"{args.problem}_N{N}_B{B}")
     result = {
@@ -214,15 +257,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": f"synthetic: first Newton iterate (bp=0.1) of random-start {args.problem} "
                 "problems, linearised on device",
-        "config": {"workload": f"{args.problem} nx={nx} nu={nu} N={N} batch={B}/GPU "
-                               f"({CONFIG_LABEL.get((args.problem, N, B), 'custom')})",
+        "config": {"workload": f"{args.problem} nx={nx} nu={nu} N={N} global batch={G} "
+                               f"({CONFIG_LABEL.get((args.problem, N, G), 'custom')}), "
+                               f"{B} per GPU",
                    "layout": args.layout,
-                   "horizon": N, "batch_per_gpu": B, "global_batch": B * world,
+                   "horizon": N, "batch_per_gpu": B, "global_batch": G,
                    "lanes_per_trajectory": lanes, "parallelism": f"trajectory-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -230,7 +274,7 @@ def main():
         "feasible_fraction": feasible_frac,
     }
     if not args.no_ipm:
-        result["ipm_solve"] = ipm_solve_rate(args.problem, N, B, rank)
+        result["ipm_solve"] = ipm_solve_rate(args.problem, N, B, rank, world)
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             sample = min(args.cpu_sample, B)

@@ -43,6 +43,24 @@
 
 namespace noc {
 
+// Diagnostic build only (-DNOC_SCAN_STAMPS, `make stamps-lib`): lane 0 of every wave of the
+// standalone scan kernel records s_memrealtime (100 MHz) and s_memtime (shader clock) at the phase
+// boundaries into a device table read back by noc_debug_scan_stamps (tools/scan_stamps.py).  The
+// stamps go to their own buffer only; no output is computed from them.
+#ifdef NOC_SCAN_STAMPS
+constexpr int kStampWaves = 65536, kStampSlots = 8;
+__device__ long long g_scan_stamps[kStampWaves][kStampSlots][2];
+#define NOC_STAMP(i)                                                                         \
+  do {                                                                                       \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < kStampWaves) {                              \
+      g_scan_stamps[blockIdx.x][i][0] = (long long)__builtin_amdgcn_s_memrealtime();         \
+      g_scan_stamps[blockIdx.x][i][1] = (long long)__builtin_amdgcn_s_memtime();             \
+    }                                                                                        \
+  } while (0)
+#else
+#define NOC_STAMP(i) do { } while (0)
+#endif
+
 template <int NX, int NU>
 struct StageData {
   Mat<NX, NX> A;
@@ -64,33 +82,47 @@ struct Elem {
   Sym<NX> J;
 };
 
-template <int NX, int NU, int L, bool AFF, bool TILED>
+// PART: 0 = the whole stage, 1 = everything but Q, 2 = Q only (phase 3 prefetches part 1 of the
+// next stage and loads Q, which the Riccati step uses last, at the top of the current one)
+template <int NX, int NU, int L, bool AFF, bool TILED, int PART = 0>
 NOC_DEV void load_stage(const KKTArgs& a, int traj, size_t si, int j, int l, int cmax, double reg,
                         StageData<NX, NU>& st) {
+  constexpr bool REST = PART != 2, WQ = PART != 1;
   if constexpr (TILED) {
-    tload<NX * NX, L>(a.A, traj, j, l, cmax, st.A.v);
-    tload<NX * NU, L>(a.Bm, traj, j, l, cmax, st.B.v);
-    tload<Sym<NX>::SZ, L>(a.Q, traj, j, l, cmax, st.Q.v);
-    tload<Sym<NU>::SZ, L>(a.R, traj, j, l, cmax, st.R.v);
-    tload<NX * NU, L>(a.M, traj, j, l, cmax, st.M.v);
-    tload<NU, L>(a.r, traj, j, l, cmax, st.r.v);
-    if constexpr (AFF) {
-      if (a.q) tload<NX, L>(a.q, traj, j, l, cmax, st.q.v); else set_zero(st.q);
-      if (a.c) tload<NX, L>(a.c, traj, j, l, cmax, st.c.v); else set_zero(st.c);
+    if constexpr (REST) {
+      tload<NX * NX, L>(a.A, traj, j, l, cmax, st.A.v);
+      tload<NX * NU, L>(a.Bm, traj, j, l, cmax, st.B.v);
+    }
+    if constexpr (WQ) tload<Sym<NX>::SZ, L>(a.Q, traj, j, l, cmax, st.Q.v);
+    if constexpr (REST) {
+      tload<Sym<NU>::SZ, L>(a.R, traj, j, l, cmax, st.R.v);
+      tload<NX * NU, L>(a.M, traj, j, l, cmax, st.M.v);
+      tload<NU, L>(a.r, traj, j, l, cmax, st.r.v);
+      if constexpr (AFF) {
+        if (a.q) tload<NX, L>(a.q, traj, j, l, cmax, st.q.v); else set_zero(st.q);
+        if (a.c) tload<NX, L>(a.c, traj, j, l, cmax, st.c.v); else set_zero(st.c);
+      }
     }
   } else {
-    gload<NX * NX>(a.A + si * (NX * NX), st.A.v);
-    gload<NX * NU>(a.Bm + si * (NX * NU), st.B.v);
-    gload_sym<NX>(a.Q + si * (NX * NX), st.Q);
-    gload_sym<NU>(a.R + si * (NU * NU), st.R);
-    gload<NX * NU>(a.M + si * (NX * NU), st.M.v);
-    gload<NU>(a.r + si * NU, st.r.v);
-    if constexpr (AFF) {
-      if (a.q) gload<NX>(a.q + si * NX, st.q.v); else set_zero(st.q);
-      if (a.c) gload<NX>(a.c + si * NX, st.c.v); else set_zero(st.c);
+    if constexpr (REST) {
+      gload<NX * NX>(a.A + si * (NX * NX), st.A.v);
+      gload<NX * NU>(a.Bm + si * (NX * NU), st.B.v);
+    }
+    if constexpr (WQ) gload_sym<NX>(a.Q + si * (NX * NX), st.Q);
+    if constexpr (REST) {
+      gload_sym<NU>(a.R + si * (NU * NU), st.R);
+      gload<NX * NU>(a.M + si * (NX * NU), st.M.v);
+      gload<NU>(a.r + si * NU, st.r.v);
+      if constexpr (AFF) {
+        if (a.q) gload<NX>(a.q + si * NX, st.q.v); else set_zero(st.q);
+        if (a.c) gload<NX>(a.c + si * NX, st.c.v); else set_zero(st.c);
+      }
     }
   }
-  NOC_UNROLL for (int i = 0; i < NU; ++i) st.R(i, i) += reg;
+  // reg is NOT added here: R + reg*I is formed where R is first used (prepend / riccati_stage),
+  // so no arithmetic waits on the R load right after it is issued and a stage's loads can be
+  // prefetched a stage ahead (phase 3)
+  (void)reg;
 }
 
 // A, B (and c) of one stage for the forward pass / map composition
@@ -139,7 +171,7 @@ NOC_DEV void load_Kd(const KKTArgs& a, int traj, size_t si, int j, int l, int cm
 
 // e <- stage (x) e   (Riccati-form prepend of one stage to the chunk element)
 template <int NX, int NU, bool AFF>
-NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st) {
+NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st, double reg) {
   Mat<NX, NX> JA;
   Mat<NX, NU> JB;
   NOC_UNROLL for (int i = 0; i < NX; ++i) {
@@ -163,7 +195,7 @@ NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st) {
   Sym<NU> W;
   NOC_UNROLL for (int i = 0; i < NU; ++i)
     NOC_UNROLL for (int j = i; j < NU; ++j) {
-      double s = st.R(i, j);
+      double s = (i == j) ? st.R(i, j) + reg : st.R(i, j);  // R + reg I (P:116-118)
       NOC_UNROLL for (int k = 0; k < NX; ++k) s += st.B(k, i) * JB(k, j);
       W(i, j) = s;
     }
@@ -368,6 +400,10 @@ struct ArgsSrc {
   NOC_DEV void stage(int s, int j, double reg, StageData<NX, NU>& st) const {
     load_stage<NX, NU, L, AFF, TILED>(a, traj, tN + s, j, l, cmax, reg, st);
   }
+  template <int PART>
+  NOC_DEV void stage_part(int s, int j, double reg, StageData<NX, NU>& st) const {
+    load_stage<NX, NU, L, AFF, TILED, PART>(a, traj, tN + s, j, l, cmax, reg, st);
+  }
   NOC_DEV void ab(int s, int j, Mat<NX, NX>& A, Mat<NX, NU>& Bm, Vec<NX>& c) const {
     load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + s, j, l, cmax, A, Bm, c);
   }
@@ -393,6 +429,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   const double reg = a.reg ? a.reg[traj] : 0.0;
   const size_t tN = (size_t)traj * N;
   const int cmax = base + (rem ? 1 : 0);
+  NOC_STAMP(0);
   StageData<NX, NU> cache[CACHE > 0 ? CACHE : 1];
   if constexpr (CACHE > 0) {
     if (a.mode != MODE_FWD) {
@@ -403,6 +440,11 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
 
   Mat<NX, NX> Phi;
   Vec<NX> phi;
+  // ablation bit 4 (timing only, results wrong): phases 3 and 4 re-read the blocks of trajectory
+  // traj & 1 instead of their own -- an L2-resident working set, so the time they lose against
+  // the full kernel is the cost of re-reading the blocks from beyond L2
+  SRC src_re = src;
+  if (a.ablate & 16) { src_re.traj = traj & 1; src_re.tN = (size_t)(traj & 1) * N; }
   if (a.mode != MODE_FWD) {
     // ---------------- phase 1: in-chunk element ----------------
     Elem<NX> e;
@@ -420,14 +462,15 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     }
     if constexpr (CACHE > 0) {
       NOC_UNROLL for (int jj = CACHE - 1; jj >= 0; --jj)
-        if (jj < len) prepend<NX, NU, AFF>(e, cache[jj]);
+        if (jj < len) prepend<NX, NU, AFF>(e, cache[jj], reg);
     } else {
       for (int s = start + len - 1; s >= start; --s) {
         StageData<NX, NU> st;
         src.stage(s, s - start, reg, st);
-        prepend<NX, NU, AFF>(e, st);
+        prepend<NX, NU, AFF>(e, st, reg);
       }
     }
+    NOC_STAMP(1);
     // ---------------- phase 2: reverse Hillis-Steele across lanes ----------------
     if (!(a.ablate & 1)) {
 #pragma unroll 1
@@ -438,6 +481,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       if (a.pred) a.pred[traj] = e.J(0, 0) + e.A(0, 0) + e.C(0, 0) + e.nu[0] + e.b[0];
       return;
     }
+    NOC_STAMP(2);
     // ---------------- phase 3: in-chunk Riccati from the true boundary ----------------
     Sym<NX> S;
     Vec<NX> v;
@@ -479,7 +523,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       Sym<NU> Quu;
       NOC_UNROLL for (int i = 0; i < NU; ++i)
         NOC_UNROLL for (int j = i; j < NU; ++j) {
-          double t = st.R(i, j);
+          double t = (i == j) ? st.R(i, j) + reg : st.R(i, j);  // R + reg I (P:116-118)
           NOC_UNROLL for (int k = 0; k < NX; ++k) t += st.B(k, i) * SB(k, j);
           Quu(i, j) = t;
         }
@@ -565,9 +609,12 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       NOC_UNROLL for (int jj = CACHE - 1; jj >= 0; --jj)
         if (jj < len) riccati_stage(start + jj, cache[jj]);
     } else {
+      // not software pipelined: prefetching stage s-1 during stage s (registers) was measured
+      // slower (phase 3 44k -> 60k cycles per wave at c3: the prefetch spills, and the phase runs
+      // at the memory-side-cache rate, not at a per-stage latency, tools/scan_stamps.py)
       for (int s = start + len - 1; s >= start; --s) {
         StageData<NX, NU> st;
-        src.stage(s, s - start, reg, st);
+        src_re.stage(s, s - start, reg, st);
         riccati_stage(s, st);
       }
     }
@@ -580,6 +627,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       if (a.pred) a.pred[traj] = pred;
       if (a.feasible) a.feasible[traj] = feas;
     }
+    NOC_STAMP(3);
     if (a.mode == MODE_BWD || (a.ablate & 2)) return;
   } else {
     // MODE_FWD: gains are inputs; compose the chunk's closed-loop map from A, B, K, d
@@ -655,6 +703,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   Vec<NX> x;
   shfl_up_arr<NX>(phi.v, x.v, 1, L);
   if (l == 0) x = x0;
+  NOC_STAMP(4);
   // dx/du rows go through LDS (slot s of the trajectory's region holds K_s, d_s from phase 3 and
   // is overwritten by x_s, u_s here) and leave as whole contiguous rows: per-lane direct stores
   // would touch one cache line per lane per store instruction.
@@ -666,7 +715,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   double nK[NU * (NX + 1)];
   Vec<NX> nc;
   auto fetch = [&](int s) {
-    src.ab(s, s - start, nA, nB, nc);
+    src_re.ab(s, s - start, nA, nB, nc);
     if (kd_lds) {
       NOC_UNROLL for (int i = 0; i < NU * (NX + 1); ++i) nK[i] = slot[s * KD + i];
     } else {
@@ -717,6 +766,8 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       }
     }
   } else {
+    // one stage prefetched (a two-deep prefetch measured no faster: the propagation runs at the
+    // rate the A, B re-reads stream at, not at the per-stage latency)
     if (len > 0) fetch(start);
     for (int s = start; s < start + len; ++s) {
       const Mat<NX, NX> A = nA;
@@ -728,6 +779,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       fwd_stage(s, A, Bm, cc, Kk);
     }
   }
+  NOC_STAMP(5);
   if (!via_lds) {
     if (last && a.dx) gstore<NX>(a.dx + (tN + traj + N) * NX, x.v);
     return;
@@ -764,6 +816,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       dst[i] = slot[s * KD + NX + (i - s * NU)];
     }
   }
+  NOC_STAMP(6);
 }
 
 template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE = 0>

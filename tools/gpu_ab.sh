@@ -1,12 +1,19 @@
 #!/bin/bash
-# A/B of two library builds on one box: B=1 pendulum and cart-pole runtime sweeps.
+# A/B of two builds of libnoc_hip.so: ip-parallel-optimal-control_amd/noc/_lib/libnoc_hip_old.so
+# (old) vs the default library (new), interleaved bench lines per config; then the KKT/golden GPU
+# tests on the new build.  Usage: tools/gpu_ab.sh [configs...]  (c2 c3 c5 n300)
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"; O=gpurun_out/ab; mkdir -p $O
+export TMPDIR=/tmp
 L="$R/ip-parallel-optimal-control_amd/noc/_lib"
 run() { local t=$1; local log=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$log" 2>&1; local rc=$?; echo "rc=$rc $log"; if [ $rc -ne 0 ]; then exit $rc; fi; }
-NOC_HIP_LIB=$L/libnoc_hip_old.so run 300 old_pend.log python tools/runtime_sweep.py --problem pendulum --out $O/old
-run 300 new_pend.log python tools/runtime_sweep.py --problem pendulum --out $O/new
-NOC_HIP_LIB=$L/libnoc_hip_old.so run 300 old_pend2.log python tools/runtime_sweep.py --problem pendulum --out $O/old2
-run 300 new_pend2.log python tools/runtime_sweep.py --problem pendulum --out $O/new2
-NOC_HIP_LIB=$L/libnoc_hip_old.so run 300 old_cart.log python tools/runtime_sweep.py --problem cartpole --out $O/old --max-n 400
-run 300 new_cart.log python tools/runtime_sweep.py --problem cartpole --out $O/new --max-n 400
+B="--steps 50 --warmup 5 --no-cpu --no-ipm"
+declare -A ARGS=([c2]="--problem pendulum --horizon 100 --batch 1024" [c3]="" [c5]="--batch 8192" [n300]="--horizon 300" [c4]="--problem linear8 --horizon 512 --batch 16384")
+CFGS="${@:-c3 c2}"
+for i in 1 2; do
+  for c in $CFGS; do
+    NOC_HIP_LIB=$L/libnoc_hip_old.so run 200 old_${c}_$i.log python bench.py $B ${ARGS[$c]}
+    run 200 new_${c}_$i.log python bench.py $B ${ARGS[$c]}
+  done
+done
+run 600 pytest_kkt.log python -u -m pytest tests/test_kkt_gpu.py tests/test_golden_gpu.py tests/test_ipm_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread

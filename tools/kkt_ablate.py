@@ -16,7 +16,7 @@ tb = blk["tiled"]
 lib = _lib.load()
 out = lqt.kkt_solve_tiled(tb, reg=blk["reg"], want_gains=False)
 variants = {"full": 0, "streamed": 8, "no_fwd": 2, "no_scan": 1, "no_scan_no_fwd": 3,
-            "phase1_only": 5, "phase1+2": 4}
+            "phase1_only": 5, "phase1+2": 4, "hot_rereads": 16}
 REPS = 10
 graphs = {}
 side = torch.cuda.Stream()
