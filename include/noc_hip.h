@@ -119,6 +119,8 @@ int noc_par_fwd_pass(int nx, int nu, int N, int B, int lanes,
 #define NOC_FAMILY_PENDULUM 1 /* examples/pendulum_runtime.py:19-72 */
 #define NOC_FAMILY_CARTPOLE 2 /* examples/cartpole_runtime.py:18-82 */
 #define NOC_FAMILY_LINEAR 3   /* examples/linear_mpc_parallel.py:24-63, linear_demo_cuda.py */
+#define NOC_FAMILY_CUSTOM 4   /* a family registered at run time (noc.families.register_family):
+                                 supported only by that family's own build of this library */
 
 #define NOC_PHASE_ROLLOUT 0
 #define NOC_PHASE_LINEARIZE 1

@@ -310,6 +310,13 @@ static hipError_t ddp_t(const noc_family& p, const DdpArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// instances for nx <= 4 only (a template: the others are never instantiated)
+template <int K, int X, int U>
+static hipError_t ddp_family(const noc_family& p, const DdpArgs& a, hipStream_t s) {
+  if constexpr (X <= 4) return ddp_t<K, X, U>(p, a, s);
+  else return hipErrorInvalidValue;
+}
+
 bool ddp_supported(const noc_family& p) {
   return family_supported(p) && p.nx <= 4;  // one wave holds the nx x nx value Hessian
 }
@@ -338,18 +345,10 @@ hipError_t ddp_solve(const noc_family& p, int N, int Bt, const double* x0, doubl
   a.iterations = iterations;
   a.passes = passes;
   a.done = done;
-  switch (p.kind) {
-    case NOC_FAMILY_PENDULUM:
-      if (p.nx == 2 && p.nu == 1) return ddp_t<NOC_FAMILY_PENDULUM, 2, 1>(p, a, s);
-      break;
-    case NOC_FAMILY_CARTPOLE:
-      if (p.nx == 4 && p.nu == 1) return ddp_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, a, s);
-      break;
-    case NOC_FAMILY_LINEAR:
-      if (p.nx == 2 && p.nu == 1) return ddp_t<NOC_FAMILY_LINEAR, 2, 1>(p, a, s);
-      break;
-    default: break;
-  }
+#define NOC_FAMILY(K, X, U) \
+  if (p.kind == K && p.nx == X && p.nu == U) return ddp_family<K, X, U>(p, a, s);
+#include NOC_FAMILIES_DEF
+#undef NOC_FAMILY
   return hipErrorInvalidValue;
 }
 

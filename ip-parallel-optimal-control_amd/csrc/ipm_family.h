@@ -10,6 +10,12 @@
 #include "../../include/noc_hip.h"
 #include "families_gen.h"
 #include "small_linalg.h"
+#ifdef NOC_CUSTOM_FAMILY
+// a custom-family build (noc.families.register_family): the generated ODE / discrete map of the
+// registered problem, its Jacobian and lambda-contracted Hessian (noc/_codegen.py), found first
+// on the include path
+#include "custom_family_gen.h"
+#endif
 
 namespace noc {
 
@@ -26,6 +32,36 @@ struct Fam {
   const noc_family& p;
   NOC_DEV explicit Fam(const noc_family& prm) : p(prm) {}
 
+  // A registered custom family either gives a continuous-time ODE (Euler-discretised here like
+  // the built-ins, noc/utils.py:50-54) or the discrete map x+ = F(x, u) itself (kDiscrete).
+#ifdef NOC_CUSTOM_FAMILY
+  static constexpr bool kDiscrete = (KIND == NOC_FAMILY_CUSTOM) && gen::kCustomDiscrete;
+#else
+  static constexpr bool kDiscrete = false;
+#endif
+  // generated right-hand side / Jacobian J = d rhs / d[x; u] / lambda-contracted Hessian
+  NOC_DEV static void rhs(const double* x, const double* u, double* f) {
+    if constexpr (KIND == NOC_FAMILY_PENDULUM) gen::pendulum_ode(x, u, f);
+    else if constexpr (KIND == NOC_FAMILY_CARTPOLE) gen::cartpole_ode(x, u, f);
+#ifdef NOC_CUSTOM_FAMILY
+    else if constexpr (KIND == NOC_FAMILY_CUSTOM) gen::custom_ode(x, u, f);
+#endif
+  }
+  NOC_DEV static void rhs_jac(const double* x, const double* u, double* J) {
+    if constexpr (KIND == NOC_FAMILY_PENDULUM) gen::pendulum_ode_jac(x, u, J);
+    else if constexpr (KIND == NOC_FAMILY_CARTPOLE) gen::cartpole_ode_jac(x, u, J);
+#ifdef NOC_CUSTOM_FAMILY
+    else if constexpr (KIND == NOC_FAMILY_CUSTOM) gen::custom_ode_jac(x, u, J);
+#endif
+  }
+  NOC_DEV static void rhs_hess_l(const double* x, const double* u, const double* l, double* H) {
+    if constexpr (KIND == NOC_FAMILY_PENDULUM) gen::pendulum_ode_hess_l(x, u, l, H);
+    else if constexpr (KIND == NOC_FAMILY_CARTPOLE) gen::cartpole_ode_hess_l(x, u, l, H);
+#ifdef NOC_CUSTOM_FAMILY
+    else if constexpr (KIND == NOC_FAMILY_CUSTOM) gen::custom_ode_hess_l(x, u, l, H);
+#endif
+  }
+
   // ------------------------------------------------------------------ dynamics
   NOC_DEV void step(const double* x, const double* u, double* xn) const {
     if constexpr (KIND == NOC_FAMILY_LINEAR) {
@@ -35,10 +71,11 @@ struct Fam {
         NOC_UNROLL for (int j = 0; j < NU; ++j) t += p.B[i * NU + j] * u[j];
         xn[i] = t;
       }
+    } else if constexpr (kDiscrete) {
+      rhs(x, u, xn);
     } else {
       double f[NX];
-      if constexpr (KIND == NOC_FAMILY_PENDULUM) gen::pendulum_ode(x, u, f);
-      else gen::cartpole_ode(x, u, f);
+      rhs(x, u, f);
       NOC_UNROLL for (int i = 0; i < NX; ++i) xn[i] = x[i] + p.dt * f[i];  // noc/utils.py:50-54
     }
   }
@@ -49,11 +86,15 @@ struct Fam {
     } else {
       constexpr int NZ = NX + NU;
       double J[NX * NZ];
-      if constexpr (KIND == NOC_FAMILY_PENDULUM) gen::pendulum_ode_jac(x, u, J);
-      else gen::cartpole_ode_jac(x, u, J);
+      rhs_jac(x, u, J);
       NOC_UNROLL for (int i = 0; i < NX; ++i) {
-        NOC_UNROLL for (int j = 0; j < NX; ++j) fx[i * NX + j] = (i == j ? 1.0 : 0.0) + p.dt * J[i * NZ + j];
-        NOC_UNROLL for (int j = 0; j < NU; ++j) fu[i * NU + j] = p.dt * J[i * NZ + NX + j];
+        if constexpr (kDiscrete) {
+          NOC_UNROLL for (int j = 0; j < NX; ++j) fx[i * NX + j] = J[i * NZ + j];
+          NOC_UNROLL for (int j = 0; j < NU; ++j) fu[i * NU + j] = J[i * NZ + NX + j];
+        } else {
+          NOC_UNROLL for (int j = 0; j < NX; ++j) fx[i * NX + j] = (i == j ? 1.0 : 0.0) + p.dt * J[i * NZ + j];
+          NOC_UNROLL for (int j = 0; j < NU; ++j) fu[i * NU + j] = p.dt * J[i * NZ + NX + j];
+        }
       }
     }
   }
@@ -63,14 +104,14 @@ struct Fam {
     if constexpr (KIND != NOC_FAMILY_LINEAR) {
       constexpr int NZ = NX + NU;
       double H[NZ * NZ];
-      if constexpr (KIND == NOC_FAMILY_PENDULUM) gen::pendulum_ode_hess_l(x, u, lam, H);
-      else gen::cartpole_ode_hess_l(x, u, lam, H);
+      rhs_hess_l(x, u, lam, H);
+      const double s = kDiscrete ? 1.0 : p.dt;
       NOC_UNROLL for (int i = 0; i < NX; ++i) {
-        NOC_UNROLL for (int j = 0; j < NX; ++j) Hxx[i * NX + j] += p.dt * H[i * NZ + j];
-        NOC_UNROLL for (int j = 0; j < NU; ++j) Hxu[i * NU + j] += p.dt * H[i * NZ + NX + j];
+        NOC_UNROLL for (int j = 0; j < NX; ++j) Hxx[i * NX + j] += s * H[i * NZ + j];
+        NOC_UNROLL for (int j = 0; j < NU; ++j) Hxu[i * NU + j] += s * H[i * NZ + NX + j];
       }
       NOC_UNROLL for (int i = 0; i < NU; ++i)
-        NOC_UNROLL for (int j = 0; j < NU; ++j) Huu[i * NU + j] += p.dt * H[(NX + i) * NZ + NX + j];
+        NOC_UNROLL for (int j = 0; j < NU; ++j) Huu[i * NU + j] += s * H[(NX + i) * NZ + NX + j];
     }
   }
 

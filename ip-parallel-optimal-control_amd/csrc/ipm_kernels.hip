@@ -438,56 +438,30 @@ static hipError_t trial_t(const noc_family& p, const noc_ipm_ws& w, int mode, hi
   return hipGetLastError();
 }
 
+// family dispatch: one instantiation per NOC_FAMILY line of families.def
 hipError_t ipm_prepare(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                        hipStream_t s) {
-  switch (p.kind) {
-    case NOC_FAMILY_PENDULUM:
-      if (p.nx == 2 && p.nu == 1) return prepare_t<NOC_FAMILY_PENDULUM, 2, 1>(p, w, mode, terminal, s);
-      break;
-    case NOC_FAMILY_CARTPOLE:
-      if (p.nx == 4 && p.nu == 1) return prepare_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, w, mode, terminal, s);
-      break;
-    case NOC_FAMILY_LINEAR:
-      if (p.nx == 2 && p.nu == 1) return prepare_t<NOC_FAMILY_LINEAR, 2, 1>(p, w, mode, terminal, s);
-      if (p.nx == 8 && p.nu == 4) return prepare_t<NOC_FAMILY_LINEAR, 8, 4>(p, w, mode, terminal, s);
-      break;
-    default: break;
-  }
+#define NOC_FAMILY(K, X, U) \
+  if (p.kind == K && p.nx == X && p.nu == U) return prepare_t<K, X, U>(p, w, mode, terminal, s);
+#include NOC_FAMILIES_DEF
+#undef NOC_FAMILY
   return hipErrorInvalidValue;
 }
 
 hipError_t ipm_rollout(const noc_family& p, const noc_ipm_ws& w, hipStream_t s) {
-  switch (p.kind) {
-    case NOC_FAMILY_PENDULUM:
-      if (p.nx == 2 && p.nu == 1) return rollout_t<NOC_FAMILY_PENDULUM, 2, 1>(p, w, s, 0);
-      break;
-    case NOC_FAMILY_CARTPOLE:
-      if (p.nx == 4 && p.nu == 1) return rollout_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, w, s, 0);
-      break;
-    case NOC_FAMILY_LINEAR:
-      if (p.nx == 2 && p.nu == 1) return rollout_t<NOC_FAMILY_LINEAR, 2, 1>(p, w, s, 0);
-      if (p.nx == 8 && p.nu == 4) return rollout_t<NOC_FAMILY_LINEAR, 8, 4>(p, w, s, 0);
-      break;
-    default: break;
-  }
+#define NOC_FAMILY(K, X, U) \
+  if (p.kind == K && p.nx == X && p.nu == U) return rollout_t<K, X, U>(p, w, s, 0);
+#include NOC_FAMILIES_DEF
+#undef NOC_FAMILY
   return hipErrorInvalidValue;
 }
 
 hipError_t ipm_prepare_main(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                             hipStream_t s) {
-  switch (p.kind) {
-    case NOC_FAMILY_PENDULUM:
-      if (p.nx == 2 && p.nu == 1) return prepare_main_t<NOC_FAMILY_PENDULUM, 2, 1>(p, w, mode, terminal, s);
-      break;
-    case NOC_FAMILY_CARTPOLE:
-      if (p.nx == 4 && p.nu == 1) return prepare_main_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, w, mode, terminal, s);
-      break;
-    case NOC_FAMILY_LINEAR:
-      if (p.nx == 2 && p.nu == 1) return prepare_main_t<NOC_FAMILY_LINEAR, 2, 1>(p, w, mode, terminal, s);
-      if (p.nx == 8 && p.nu == 4) return prepare_main_t<NOC_FAMILY_LINEAR, 8, 4>(p, w, mode, terminal, s);
-      break;
-    default: break;
-  }
+#define NOC_FAMILY(K, X, U) \
+  if (p.kind == K && p.nx == X && p.nu == U) return prepare_main_t<K, X, U>(p, w, mode, terminal, s);
+#include NOC_FAMILIES_DEF
+#undef NOC_FAMILY
   return hipErrorInvalidValue;
 }
 
@@ -497,19 +471,10 @@ hipError_t ipm_promote(const noc_ipm_ws& w, hipStream_t s) {
 }
 
 hipError_t ipm_trial(const noc_family& p, const noc_ipm_ws& w, int mode, hipStream_t s) {
-  switch (p.kind) {
-    case NOC_FAMILY_PENDULUM:
-      if (p.nx == 2 && p.nu == 1) return trial_t<NOC_FAMILY_PENDULUM, 2, 1>(p, w, mode, s);
-      break;
-    case NOC_FAMILY_CARTPOLE:
-      if (p.nx == 4 && p.nu == 1) return trial_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, w, mode, s);
-      break;
-    case NOC_FAMILY_LINEAR:
-      if (p.nx == 2 && p.nu == 1) return trial_t<NOC_FAMILY_LINEAR, 2, 1>(p, w, mode, s);
-      if (p.nx == 8 && p.nu == 4) return trial_t<NOC_FAMILY_LINEAR, 8, 4>(p, w, mode, s);
-      break;
-    default: break;
-  }
+#define NOC_FAMILY(K, X, U) \
+  if (p.kind == K && p.nx == X && p.nu == U) return trial_t<K, X, U>(p, w, mode, s);
+#include NOC_FAMILIES_DEF
+#undef NOC_FAMILY
   return hipErrorInvalidValue;
 }
 
@@ -519,12 +484,11 @@ hipError_t ipm_init(const noc_ipm_ws& w, double bp0, hipStream_t s) {
 }
 
 bool family_supported(const noc_family& p) {
-  switch (p.kind) {
-    case NOC_FAMILY_PENDULUM: return p.nx == 2 && p.nu == 1;
-    case NOC_FAMILY_CARTPOLE: return p.nx == 4 && p.nu == 1;
-    case NOC_FAMILY_LINEAR: return (p.nx == 2 && p.nu == 1) || (p.nx == 8 && p.nu == 4);
-    default: return false;
-  }
+#define NOC_FAMILY(K, X, U) \
+  if (p.kind == K && p.nx == X && p.nu == U) return true;
+#include NOC_FAMILIES_DEF
+#undef NOC_FAMILY
+  return false;
 }
 
 }  // namespace noc

@@ -514,26 +514,35 @@ int debug_phase_cycles(long long* out, int n, int reset) {
   return 0;
 }
 
+// persistent instances exist for the families with nx <= 4 (an nx = 8 scan element does not fit a
+// wave's registers next to the solver state: those run the launch-per-phase driver)
+template <int NX>
+constexpr bool persistent_instance() { return NX <= 4; }
+
 bool ipm_solve_supported(const noc_family& p, int N, int lanes) {
   if (lanes != PL || !family_supported(p)) return false;
-  if (p.kind == NOC_FAMILY_LINEAR && p.nx == 8) return false;  // no nx=8 persistent instance
-  return solve_lds_bytes(p.nx, p.nu, N) > 0;
+  bool inst = false;
+#define NOC_FAMILY(K, X, U) \
+  if (p.kind == K && p.nx == X && p.nu == U) inst = persistent_instance<X>();
+#include NOC_FAMILIES_DEF
+#undef NOC_FAMILY
+  return inst && solve_lds_bytes(p.nx, p.nu, N) > 0;
+}
+
+template <int K, int X, int U>
+static hipError_t solve_family(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                               double bp0, int max_solves, hipStream_t s) {
+  if constexpr (persistent_instance<X>()) return solve_t<K, X, U>(p, w, mode, terminal, bp0, max_solves, s);
+  else return hipErrorInvalidValue;
 }
 
 hipError_t ipm_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal, double bp0,
                      int max_solves, hipStream_t s) {
-  switch (p.kind) {
-    case NOC_FAMILY_PENDULUM:
-      if (p.nx == 2 && p.nu == 1) return solve_t<NOC_FAMILY_PENDULUM, 2, 1>(p, w, mode, terminal, bp0, max_solves, s);
-      break;
-    case NOC_FAMILY_CARTPOLE:
-      if (p.nx == 4 && p.nu == 1) return solve_t<NOC_FAMILY_CARTPOLE, 4, 1>(p, w, mode, terminal, bp0, max_solves, s);
-      break;
-    case NOC_FAMILY_LINEAR:
-      if (p.nx == 2 && p.nu == 1) return solve_t<NOC_FAMILY_LINEAR, 2, 1>(p, w, mode, terminal, bp0, max_solves, s);
-      break;
-    default: break;
-  }
+#define NOC_FAMILY(K, X, U)                                                              \
+  if (p.kind == K && p.nx == X && p.nu == U)                                             \
+    return solve_family<K, X, U>(p, w, mode, terminal, bp0, max_solves, s);
+#include NOC_FAMILIES_DEF
+#undef NOC_FAMILY
   return hipErrorInvalidValue;
 }
 

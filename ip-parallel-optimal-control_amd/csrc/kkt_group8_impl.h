@@ -352,7 +352,7 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
   }
 }
 
-static hipError_t launch_kkt_group8(const KKTArgs& a, hipStream_t stream) {
+[[maybe_unused]] static hipError_t launch_kkt_group8(const KKTArgs& a, hipStream_t stream) {
   if (!a.K || !a.d) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.B + g8::TPW - 1) / g8::TPW);
   const bool aff = a.q || a.c || a.p;

@@ -2,7 +2,8 @@
 #include "kkt_scan_impl.h"
 
 namespace noc {
-hipError_t kkt_dispatch_2x1(const KKTArgs& a, int lanes, hipStream_t stream) {
+template <>
+hipError_t kkt_dispatch_shape<2, 1>(const KKTArgs& a, int lanes, hipStream_t stream) {
   return dispatch_aff<2, 1>(a, lanes, stream);
 }
 }  // namespace noc

@@ -2,7 +2,8 @@
 #include "kkt_scan_impl.h"
 
 namespace noc {
-hipError_t kkt_dispatch_4x1(const KKTArgs& a, int lanes, hipStream_t stream) {
+template <>
+hipError_t kkt_dispatch_shape<4, 1>(const KKTArgs& a, int lanes, hipStream_t stream) {
   return dispatch_aff<4, 1>(a, lanes, stream);
 }
 }  // namespace noc

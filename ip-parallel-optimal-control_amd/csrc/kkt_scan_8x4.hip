@@ -2,7 +2,8 @@
 #include "kkt_scan_impl.h"
 
 namespace noc {
-hipError_t kkt_dispatch_8x4(const KKTArgs& a, int lanes, hipStream_t stream) {
+template <>
+hipError_t kkt_dispatch_shape<8, 4>(const KKTArgs& a, int lanes, hipStream_t stream) {
   return dispatch_aff<8, 4>(a, lanes, stream);
 }
 }  // namespace noc

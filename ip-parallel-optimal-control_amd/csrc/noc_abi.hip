@@ -9,6 +9,10 @@
 #include "noc_internal.h"
 #include "small_linalg.h"
 
+namespace noc {
+static std::string kkt_shapes_str();
+}
+
 namespace {
 thread_local std::string g_last_error;
 int g_ablate = 0;  // timing-only phase ablation (noc_debug_set_ablation); never set in product use
@@ -35,7 +39,7 @@ int hip_status(hipError_t e, const char* where) {
 int check_dims(int nx, int nu, int N, int B, int lanes) {
   if (!noc::kkt_supported(nx, nu))
     return fail(-1, "unsupported (nx, nu) = (" + std::to_string(nx) + ", " + std::to_string(nu) +
-                        "); supported: (2,1) (4,1) (8,4)");
+                        "); supported: " + noc::kkt_shapes_str());
   if (N < 1) return fail(-1, "horizon N must be >= 1");
   if (B < 0) return fail(-1, "batch B must be >= 0");
   if (lanes != 0 && lanes != 1 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64)
@@ -46,14 +50,25 @@ int check_dims(int nx, int nu, int N, int B, int lanes) {
 
 namespace noc {
 bool kkt_supported(int nx, int nu) {
-  return (nx == 2 && nu == 1) || (nx == 4 && nu == 1) || (nx == 8 && nu == 4);
+#define NOC_KKT_SHAPE(X, U) if (nx == X && nu == U) return true;
+#include NOC_KKT_SHAPES_DEF
+#undef NOC_KKT_SHAPE
+  return false;
+}
+
+static std::string kkt_shapes_str() {
+  std::string s;
+#define NOC_KKT_SHAPE(X, U) s += std::string(s.empty() ? "" : " ") + "(" #X "," #U ")";
+#include NOC_KKT_SHAPES_DEF
+#undef NOC_KKT_SHAPE
+  return s;
 }
 
 hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t stream) {
   if (lanes == 1) return kkt_group_dispatch(nx, nu, a, stream);
-  if (nx == 2 && nu == 1) return kkt_dispatch_2x1(a, lanes, stream);
-  if (nx == 4 && nu == 1) return kkt_dispatch_4x1(a, lanes, stream);
-  if (nx == 8 && nu == 4) return kkt_dispatch_8x4(a, lanes, stream);
+#define NOC_KKT_SHAPE(X, U) if (nx == X && nu == U) return kkt_dispatch_shape<X, U>(a, lanes, stream);
+#include NOC_KKT_SHAPES_DEF
+#undef NOC_KKT_SHAPE
   return hipErrorInvalidValue;
 }
 
@@ -163,6 +178,8 @@ static int kkt_common(int mode, int tiled, int nx, int nu, int N, int B, int lan
   if (tiled && lanes == 0) return fail(-1, "the tiled layout needs an explicit lanes value");
   if (tiled && lanes == 1 && !(nx == 8 && nu == 4))
     return fail(-1, "the grouped (lanes = 1) tiled layout is supported for (nx, nu) = (8, 4)");
+  if (lanes == 1 && !(64 % nx == 0 && nu <= nx))
+    return fail(-1, "the group solve (lanes = 1) needs nx dividing 64 and nu <= nx");
   (void)bwd;
   (void)fwd;
   const int L = lanes ? lanes : noc::kkt_default_lanes(nx, nu, N);

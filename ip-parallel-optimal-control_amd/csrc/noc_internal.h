@@ -4,6 +4,16 @@
 
 #include "../../include/noc_hip.h"
 
+// The family / KKT-shape lists the dispatchers expand (X-macros).  A custom-family build points
+// these at its generated lists (an absolute path: a quoted include would otherwise find the
+// default list next to the source first).
+#ifndef NOC_FAMILIES_DEF
+#define NOC_FAMILIES_DEF "families.def"
+#endif
+#ifndef NOC_KKT_SHAPES_DEF
+#define NOC_KKT_SHAPES_DEF "kkt_shapes.def"
+#endif
+
 namespace noc {
 
 enum KKTMode : int { MODE_FULL = 0, MODE_BWD = 1, MODE_FWD = 2 };
@@ -33,9 +43,10 @@ inline size_t kkt_lds_bytes_rt(int nx, int nu, int N, int L) {
 hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t stream);
 // lanes == 1: horizon-sequential solve, one trajectory per nx-lane group (kkt_group_impl.h)
 hipError_t kkt_group_dispatch(int nx, int nu, const KKTArgs& a, hipStream_t stream);
-hipError_t kkt_dispatch_2x1(const KKTArgs& a, int lanes, hipStream_t stream);
-hipError_t kkt_dispatch_4x1(const KKTArgs& a, int lanes, hipStream_t stream);
-hipError_t kkt_dispatch_8x4(const KKTArgs& a, int lanes, hipStream_t stream);
+// the scan for one (nx, nu) of kkt_shapes.def; instantiated in that shape's translation unit
+// (kkt_scan_<nx>x<nu>.hip, or csrc/custom/kkt_scan_custom.hip in a custom-family build)
+template <int NX, int NU>
+hipError_t kkt_dispatch_shape(const KKTArgs& a, int lanes, hipStream_t stream);
 bool kkt_supported(int nx, int nu);
 int kkt_default_lanes(int nx, int nu, int N);
 int kkt_pick_lanes(int nx, int nu, int N, int B);

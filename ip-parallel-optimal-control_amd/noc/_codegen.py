@@ -1,0 +1,111 @@
+"""Device code generation for problem families: sympy expressions of an ODE right-hand side (or a
+discrete map) -> straight-line fp64 HIP device functions for the value, the Jacobian with respect
+to z = [x; u] and the lambda-contracted Hessian sum_i l_i d2 f_i / dz dz, with common
+subexpressions eliminated and sin/cos of a state computed once with sincos().
+
+Used by tools/gen_family_derivs.py (the built-in families -> csrc/families_gen.h, committed) and
+by noc.families.register_family (user families -> a per-family build of libnoc_hip.so).  This is
+what the reference gets from jax.jacrev / jax.hessian on the Python dynamics
+(noc/par_interior_point_newton.py:13-28): the derivatives are exact symbolic ones, evaluated on
+the device.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import numpy as np
+import sympy as sp
+
+
+def _trig_subst(exprs, X):
+    """Replace sin(x_i)/cos(x_i) by symbols computed once with sincos() (shared range reduction:
+    the rollout's dependent chain is dominated by fp64 trig)."""
+    subs, pre = {}, []
+    for xi in X:
+        s_, c_ = sp.symbols(f"s_{xi} c_{xi}", real=True)
+        if any(e.has(sp.sin(xi)) or e.has(sp.cos(xi)) for e in exprs):
+            subs[sp.sin(xi)] = s_
+            subs[sp.cos(xi)] = c_
+            pre.append(f"  double {s_}, {c_};\n  sincos({xi}, &{s_}, &{c_});")
+    return [e.subs(subs) for e in exprs], pre
+
+
+def emit(name, X, U, f):
+    """Device functions {name}_ode(x, u, f), {name}_ode_jac(x, u, J) (J[i][j] = d f_i / d z_j,
+    row-major nx x (nx+nu)) and {name}_ode_hess_l(x, u, l, H) ((nx+nu) x (nx+nu), row-major)."""
+    Z = list(X) + list(U)
+    nz = len(Z)
+    nx = len(X)
+    lam = sp.symbols(f"l0:{nx}", real=True)
+    jac = [[sp.diff(fi, zj) for zj in Z] for fi in f]
+    hl = [[sum(lam[i] * sp.diff(f[i], Z[a], Z[b]) for i in range(nx)) for b in range(nz)]
+          for a in range(nz)]
+    lines = []
+
+    def block(fn_sig, exprs, targets, with_lambda=False):
+        exprs, pre = _trig_subst(exprs, X)
+        reps, red = sp.cse(exprs, symbols=sp.numbered_symbols("t"))
+        lines.append(fn_sig + " {")
+        for i in range(nx):
+            lines.append(f"  [[maybe_unused]] const double x{i} = x[{i}];")
+            if with_lambda:
+                lines.append(f"  [[maybe_unused]] const double l{i} = l[{i}];")
+        for i in range(len(U)):
+            lines.append(f"  [[maybe_unused]] const double u{i} = u[{i}];")
+        lines.extend(pre)
+        lines.extend(f"  const double {sp.ccode(s)} = {sp.ccode(e)};" for s, e in reps)
+        lines.extend(f"  {t} = {sp.ccode(e)};" for t, e in zip(targets, red))
+        lines.append("}")
+
+    block(f"NOC_DEV void {name}_ode(const double* x, const double* u, double* f)",
+          list(f), [f"f[{i}]" for i in range(nx)])
+    block(f"NOC_DEV void {name}_ode_jac(const double* x, const double* u, double* J)",
+          [jac[i][j] for i in range(nx) for j in range(nz)],
+          [f"J[{i * nz + j}]" for i in range(nx) for j in range(nz)])
+    block(f"NOC_DEV void {name}_ode_hess_l(const double* x, const double* u, const double* l, double* H)",
+          [hl[a][b] for a in range(nz) for b in range(nz)],
+          [f"H[{a * nz + b}]" for a in range(nz) for b in range(nz)], with_lambda=True)
+    return "\n".join(lines)
+
+
+# numpy ufunc name -> sympy function: numpy applies a ufunc to an object array (or a sympy scalar)
+# by calling the element's method of the same name, so while these are attached to sympy.Expr a
+# dynamics written with np.sin / np.exp / ... on numpy arrays can be called on sympy symbols.
+_UFUNCS = {"sin": sp.sin, "cos": sp.cos, "tan": sp.tan, "arcsin": sp.asin, "arccos": sp.acos,
+           "arctan": sp.atan, "sinh": sp.sinh, "cosh": sp.cosh, "tanh": sp.tanh, "exp": sp.exp,
+           "log": sp.log, "sqrt": sp.sqrt, "arctan2": None}
+
+
+@contextlib.contextmanager
+def _sympy_ufuncs():
+    saved = {k: getattr(sp.Expr, k, None) for k in _UFUNCS}
+    try:
+        for k, fn in _UFUNCS.items():
+            if fn is not None:
+                setattr(sp.Expr, k, (lambda f: lambda self: f(self))(fn))
+        sp.Expr.arctan2 = lambda self, other: sp.atan2(self, other)
+        yield
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                if k in sp.Expr.__dict__:
+                    delattr(sp.Expr, k)
+            else:
+                setattr(sp.Expr, k, v)
+
+
+def trace(fn, nx: int, nu: int):
+    """Call fn(x, u) on symbolic state / control arrays (numpy object arrays of sympy symbols
+    x0.., u0..) and return (X, U, f) with f the list of nx sympy expressions.  fn may be written
+    with numpy (np.sin, np.hstack, @, ...) exactly like the reference examples' dynamics."""
+    X = list(sp.symbols(f"x0:{nx}", real=True))
+    U = list(sp.symbols(f"u0:{nu}", real=True))
+    with _sympy_ufuncs():
+        out = fn(np.array(X, dtype=object), np.array(U, dtype=object))
+    out = [sp.sympify(e) for e in np.asarray(out, dtype=object).reshape(-1)]
+    if len(out) != nx:
+        raise ValueError(f"the dynamics returned {len(out)} components, expected nx = {nx}")
+    free = set().union(*(e.free_symbols for e in out)) - set(X) - set(U)
+    if free:
+        raise ValueError(f"the dynamics depend on symbols other than the state / control: {free}")
+    return X, U, out

@@ -34,7 +34,7 @@ SIGNATURES = {
 }
 
 # --- structs of include/noc_hip.h --------------------------------------------------------------
-FAMILY_PENDULUM, FAMILY_CARTPOLE, FAMILY_LINEAR = 1, 2, 3
+FAMILY_PENDULUM, FAMILY_CARTPOLE, FAMILY_LINEAR, FAMILY_CUSTOM = 1, 2, 3, 4
 PHASE_ROLLOUT, PHASE_LINEARIZE, PHASE_SOLVE, PHASE_DONE, PHASE_ROLLED = 0, 1, 2, 3, 4
 PHASE_ROLLOUT_PENDING = 5
 MODE_PAR, MODE_SEQ = 0, 1
@@ -81,10 +81,22 @@ SIGNATURES.update({
 })
 
 _lib: Optional[ctypes.CDLL] = None
+_family_libs = {}   # path -> CDLL of a registered custom family's build (noc.families)
+_shape_libs = {}    # (nx, nu) -> CDLL of a custom build that instantiates that KKT shape
 
 
 class NocError(RuntimeError):
     pass
+
+
+def _typed(lib: ctypes.CDLL) -> ctypes.CDLL:
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.noc_abi_version() != 1:
+        raise NocError("libnoc_hip.so ABI version mismatch")
+    return lib
 
 
 def load(path: Optional[str] = None) -> ctypes.CDLL:
@@ -96,21 +108,41 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     if not os.path.exists(p):
         raise NocError(f"libnoc_hip.so not found at {p}; build it with "
                        f"`make -C ip-parallel-optimal-control_amd -j8`")
-    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
-    for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
-        fn.restype = res
-        fn.argtypes = args
-    if lib.noc_abi_version() != 1:
-        raise NocError("libnoc_hip.so ABI version mismatch")
+    lib = _typed(ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL))
     if path is None:
         _lib = lib
     return lib
 
 
-def check(rc: int, what: str) -> None:
+def load_for(family) -> ctypes.CDLL:
+    """The library that implements `family`: the default build for the built-in families, the
+    family's own build (noc.families.register_family) for a registered one."""
+    path = getattr(family, "lib_path", None)
+    if not path:
+        return load()
+    lib = _family_libs.get(path)
+    if lib is None:
+        if not os.path.exists(path):
+            raise NocError(f"the library of family '{getattr(family, 'name', '?')}' is not built "
+                           f"({path}); call noc.families.register_family(..., build=True)")
+        lib = _typed(ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL))
+        _family_libs[path] = lib
+        _shape_libs.setdefault((int(family.nx), int(family.nu)), lib)
+    return lib
+
+
+def for_shape(nx: int, nu: int) -> ctypes.CDLL:
+    """The library whose KKT solve covers (nx, nu): the default build's shapes, else a loaded
+    custom family's."""
+    lib = load()
+    if lib.noc_kkt_supported(int(nx), int(nu)) == 1:
+        return lib
+    return _shape_libs.get((int(nx), int(nu)), lib)  # the default reports the unsupported shape
+
+
+def check(rc: int, what: str, lib: Optional[ctypes.CDLL] = None) -> None:
     if rc != 0:
-        msg = load().noc_last_error().decode(errors="replace")
+        msg = (lib or load()).noc_last_error().decode(errors="replace")
         raise NocError(f"{what} failed (rc={rc}): {msg}")
 
 

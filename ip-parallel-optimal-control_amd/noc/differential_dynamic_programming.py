@@ -28,7 +28,7 @@ def interior_point_ddp(ocp: OCP, controls, initial_state, device="cuda", bp0: fl
     if ocp.family is None:
         raise _lib.NocError("OCP has no registered device family (use noc.problems.*): the HIP "
                             "kernels cannot evaluate Python callables")
-    lib = _lib.load()
+    lib = _lib.load_for(ocp.family)
     fam = ocp.family.to_c()
     if not lib.noc_ddp_supported(ctypes.byref(fam)):
         raise _lib.NocError("interior-point DDP supports the registered families with nx <= 4")
@@ -51,7 +51,7 @@ def interior_point_ddp(ocp: OCP, controls, initial_state, device="cuda", bp0: fl
     _lib.check(lib.noc_ddp_solve(ctypes.byref(fam), N, Bt, _lib.ptr(X0), _lib.ptr(U),
                                  _lib.ptr(work), _lib.ptr(its), _lib.ptr(passes), _lib.ptr(done),
                                  float(bp0), int(max_passes), _lib.stream_handle(dev)),
-               "noc_ddp_solve")
+               "noc_ddp_solve", lib)
     Uh, itn = U.cpu().numpy(), its.cpu().numpy()
     info = dict(passes=passes.cpu().numpy(), done=done.cpu().numpy().astype(bool),
                 states=work[:Bt * (N + 1) * nx].view(Bt, N + 1, nx).cpu().numpy())

@@ -26,7 +26,7 @@ def default_terminal(mode: int) -> int:
 
 def persistent_supported(family, N: int) -> bool:
     """noc_ipm_solve_supported: the whole-solve kernel handles this family / horizon (lanes 64)."""
-    lib = _lib.load()
+    lib = _lib.load_for(family)
     return lib.noc_ipm_solve_supported(ctypes.byref(family.to_c()), int(N), 64) == 1
 
 
@@ -42,7 +42,7 @@ class BatchedIPM:
         self.N, self.Bt = int(N), int(batch)
         self.nx, self.nu = family.nx, family.nu
         self.device = torch.device(device)
-        lib = _lib.load()
+        lib = _lib.load_for(family)
         self.persistent = bool(persistent)
         if self.persistent:
             if lanes not in (0, 64) or not persistent_supported(family, N):
@@ -99,13 +99,13 @@ class BatchedIPM:
 
     def init(self, bp0: float = 0.1):
         _lib.check(self._lib.noc_ipm_init(ctypes.byref(self.ws), float(bp0), self._stream()),
-                   "noc_ipm_init")
+                   "noc_ipm_init", self._lib)
         if self.overlap:  # the roll stream must see load() + init() before its first rollout
             self.ev_main.record(torch.cuda.current_stream(self.device))
 
     def prepare(self, mode: int, terminal: int):
         _lib.check(self._lib.noc_ipm_prepare(ctypes.byref(self.fam_c), ctypes.byref(self.ws), mode,
-                                             terminal, self._stream()), "noc_ipm_prepare")
+                                             terminal, self._stream()), "noc_ipm_prepare", self._lib)
 
     def step(self, mode: int, terminal: int):
         """One device iteration.  With overlap (default) the rollouts of trajectories that start
@@ -113,20 +113,20 @@ class BatchedIPM:
         if not self.overlap:
             _lib.check(self._lib.noc_ipm_step(ctypes.byref(self.fam_c), ctypes.byref(self.ws),
                                               mode, terminal, self.lanes, self._stream()),
-                       "noc_ipm_step")
+                       "noc_ipm_step", self._lib)
             return
         main = torch.cuda.current_stream(self.device)
         roll = self.roll_stream
         roll.wait_event(self.ev_main)
         _lib.check(self._lib.noc_ipm_rollout(ctypes.byref(self.fam_c), ctypes.byref(self.ws),
-                                             roll.cuda_stream), "noc_ipm_rollout")
+                                             roll.cuda_stream), "noc_ipm_rollout", self._lib)
         self.ev_roll.record(roll)
         _lib.check(self._lib.noc_ipm_step_main(ctypes.byref(self.fam_c), ctypes.byref(self.ws),
                                                mode, terminal, main.cuda_stream),
-                   "noc_ipm_step_main")
+                   "noc_ipm_step_main", self._lib)
         main.wait_event(self.ev_roll)
         _lib.check(self._lib.noc_ipm_promote(ctypes.byref(self.ws), main.cuda_stream),
-                   "noc_ipm_promote")
+                   "noc_ipm_promote", self._lib)
         self.ev_main.record(main)
 
     def active_count(self) -> int:
@@ -147,7 +147,7 @@ class BatchedIPM:
         terminal = default_terminal(mode) if terminal is None else terminal
         _lib.check(self._lib.noc_ipm_solve(ctypes.byref(self.fam_c), ctypes.byref(self.ws), mode,
                                            terminal, float(bp0), int(max_solves), self._stream()),
-                   "noc_ipm_solve")
+                   "noc_ipm_solve", self._lib)
         return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
 
     def solve(self, mode: int = _lib.MODE_PAR, terminal: Optional[int] = None,

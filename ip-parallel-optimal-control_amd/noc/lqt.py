@@ -53,14 +53,15 @@ def _batched(*ts):
 
 def pick_lanes(nx: int, nu: int, N: int, B: int) -> int:
     """Batch-aware lanes per trajectory for B trajectories (noc_kkt_pick_lanes)."""
-    L = _lib.load().noc_kkt_pick_lanes(nx, nu, N, B)
-    _lib.check(0 if L > 0 else L, "noc_kkt_pick_lanes")
+    lib = _lib.for_shape(nx, nu)
+    L = lib.noc_kkt_pick_lanes(nx, nu, N, B)
+    _lib.check(0 if L > 0 else L, "noc_kkt_pick_lanes", lib)
     return L
 
 
 def gains_on_chip(nx: int, nu: int, N: int, lanes: int = 0) -> bool:
     """True if the fused solve keeps K, d in LDS (noc_kkt_gains_on_chip), so they may be omitted."""
-    return _lib.load().noc_kkt_gains_on_chip(nx, nu, N, lanes) == 1
+    return _lib.for_shape(nx, nu).noc_kkt_gains_on_chip(nx, nu, N, lanes) == 1
 
 
 def kkt_solve(A, B, Q, R, M, r, P, reg=None, x0=None, q=None, c=None, p=None, active=None,
@@ -92,12 +93,12 @@ def kkt_solve(A, B, Q, R, M, r, P, reg=None, x0=None, q=None, c=None, p=None, ac
             torch.empty(Bt, N, nu, **f64) if gains else None,
             torch.empty(Bt, N + 1, nx, nx, **f64) if want_value else None,
             torch.empty(Bt, N + 1, nx, **f64) if want_value else None)
-    lib = _lib.load()
+    lib = _lib.for_shape(nx, nu)
     rc = lib.noc_kkt_solve(nx, nu, N, Bt, lanes, *(_lib.ptr(t) for t in (
         A, B, Q, R, M, r, q, c, P, p, x0, reg, active,
         out.dx, out.du, out.pred, out.feasible, out.K, out.d, out.S, out.v)),
         _lib.stream_handle(dev))
-    _lib.check(rc, "noc_kkt_solve")
+    _lib.check(rc, "noc_kkt_solve", lib)
     if squeeze:
         out = KKTResult(*(None if t is None else t[0] for t in out))
     return out
@@ -186,11 +187,12 @@ def kkt_solve_tiled(tb: TiledBlocks, reg=None, x0=None, active=None, want_value=
             torch.empty(Bt, N + 1, nx, **f64) if want_value else None)
     if active is not None:
         active = active.to(device=dev, dtype=torch.int32).contiguous()
-    rc = _lib.load().noc_kkt_solve_tiled(nx, nu, N, Bt, L, *(_lib.ptr(t) for t in (
+    lib = _lib.for_shape(nx, nu)
+    rc = lib.noc_kkt_solve_tiled(nx, nu, N, Bt, L, *(_lib.ptr(t) for t in (
         tb.A, tb.B, tb.Q, tb.R, tb.M, tb.r, None, None, tb.P, None, _c(x0, "x0"), _c(reg, "reg"),
         active, out.dx, out.du, out.pred, out.feasible, out.K, out.d, out.S, out.v)),
         _lib.stream_handle(dev))
-    _lib.check(rc, "noc_kkt_solve_tiled")
+    _lib.check(rc, "noc_kkt_solve_tiled", lib)
     return out
 
 
@@ -210,10 +212,11 @@ def bwd_pass(A, B, Q, R, M, r, P, reg=None, q=None, c=None, p=None, active=None,
     feas = torch.empty(Bt, device=A.device, dtype=torch.int32)
     if active is not None:
         active = active.to(device=A.device, dtype=torch.int32).contiguous()
-    rc = _lib.load().noc_par_bwd_pass(nx, nu, N, Bt, lanes, *(_lib.ptr(t) for t in (
+    lib = _lib.for_shape(nx, nu)
+    rc = lib.noc_par_bwd_pass(nx, nu, N, Bt, lanes, *(_lib.ptr(t) for t in (
         A, B, Q, R, M, r, q, c, P, p, reg, active, K, d, S, v, pred, feas)),
         _lib.stream_handle(A.device))
-    _lib.check(rc, "noc_par_bwd_pass")
+    _lib.check(rc, "noc_par_bwd_pass", lib)
     res = (K, d, S, v, pred, feas)
     return tuple(t[0] for t in res) if squeeze else res
 
@@ -230,9 +233,10 @@ def fwd_pass(A, B, K, d, x0=None, c=None, active=None, lanes=0):
     dx = torch.empty(Bt, N + 1, nx, **f64)
     if active is not None:
         active = active.to(device=A.device, dtype=torch.int32).contiguous()
-    rc = _lib.load().noc_par_fwd_pass(nx, nu, N, Bt, lanes, *(_lib.ptr(t) for t in (
+    lib = _lib.for_shape(nx, nu)
+    rc = lib.noc_par_fwd_pass(nx, nu, N, Bt, lanes, *(_lib.ptr(t) for t in (
         A, B, c, x0, K, d, active, du, dx)), _lib.stream_handle(A.device))
-    _lib.check(rc, "noc_par_fwd_pass")
+    _lib.check(rc, "noc_par_fwd_pass", lib)
     return (du[0], dx[0]) if squeeze else (du, dx)
 
 

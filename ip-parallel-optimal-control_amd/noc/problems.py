@@ -35,6 +35,8 @@ class Family:
     wf: List[float] = field(default_factory=list)
     A: np.ndarray = None
     B: np.ndarray = None
+    lib_path: str = None          # a registered family's own build (noc.families), else None
+    name: str = ""
 
     def to_c(self) -> _lib.NocFamily:
         c = _lib.NocFamily()
