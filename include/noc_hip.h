@@ -149,10 +149,12 @@ typedef struct noc_family {
 } noc_family;
 
 /* Workspace of device pointers (all fp64 unless noted; Bt trajectories, horizon N). */
+#define NOC_WS_ONE_STAGE 1 /* flags bit: stop after ONE barrier stage (newton_oc, P:127-225 /
+                              S:108-177) instead of running the schedule while bp > 1e-4 */
 typedef struct noc_ipm_ws {
   int Bt, N;
   int lanes;                           /* tiled layout of A,B,Q,R,M,r,K,d (8/16/32/64)  */
-  int reserved;
+  int flags;                           /* NOC_WS_* bits (0 = the whole barrier schedule) */
   double *x, *u, *x0;                  /* (Bt,N+1,nx) (Bt,N,nu) (Bt,nx)           */
   double *A, *B, *Q, *R, *M, *r, *P;   /* LQ blocks: tiled (P natural)              */
   double *cx, *cu, *lc, *lam;          /* cx, cu, lc tiled (E = nx, nu, 1); lam (Bt,N+1,nx) */
@@ -201,6 +203,31 @@ int noc_ipm_solve_supported(const noc_family* fam, int N, int lanes);
 int noc_debug_phase_cycles(long long* out, int n, int reset);
 int noc_ipm_solve(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, double bp0,
                   int max_solves, void* stream);
+
+/* ---- building blocks of one Newton step: the reference's API functions as standalone batched
+ * kernels (the fused solvers above inline them).  Natural layout, leading batch axis B. ---------
+ * compute_derivatives (P:13-28 == S:10-25, D:10-25) of a family at (x (B,N+1,nx), u (B,N,nu)),
+ * barrier parameter bp (B): cx (B,N,nx) cu (B,N,nu) cxx (B,N,nx,nx) cuu (B,N,nu,nu)
+ * cxu (B,N,nx,nu) fx (B,N,nx,nx) fu (B,N,nx,nu) fxx (B,N,nx,nx,nx) fuu (B,N,nx,nu,nu)
+ * fxu (B,N,nx,nx,nu) -- jax.grad / hessian / jacrev shapes. */
+int noc_derivatives(const noc_family* fam, int N, int B, const double* x, const double* u,
+                    const double* bp, double* cx, double* cu, double* cxx, double* cuu,
+                    double* cxu, double* fx, double* fu, double* fxx, double* fuu, double* fxu,
+                    void* stream);
+/* grad(final_cost)(xN) (B,nx) and hessian(final_cost)(xN) (B,nx,nx; NULL = skip), C:35 / S:66. */
+int noc_final_cost_derivs(const noc_family* fam, int B, const double* xN, double* grad,
+                          double* hess, void* stream);
+/* costates lambda (B,N+1,nx): lambda_N = lamT (B,nx), lambda_k = cx_k + fx_k' lambda_{k+1}.
+ * sequential = 1: seq_costates (C:43-54, one recursion per trajectory); 0: par_costates (C:34-40,
+ * the affine associative scan).  nx <= 8. */
+int noc_costates(int nx, int N, int B, const double* lamT, const double* cx, const double* fx,
+                 double* lam, int sequential, void* stream);
+/* compute_lqr_params (P:31-42 == S:28-39) with l = lambda[:, 1:]: ru (B,N,nu) = cu + fu' l,
+ * Q = cxx + l.fxx, R = cuu + l.fuu, M = cxu + l.fxu.  nx <= 8, nu <= 8. */
+int noc_lqr_params(int nx, int nu, int N, int B, const double* lam, const double* cu,
+                   const double* cxx, const double* cuu, const double* cxu, const double* fu,
+                   const double* fxx, const double* fuu, const double* fxu, double* ru, double* Q,
+                   double* R, double* M, void* stream);
 
 /* Interior-point DDP (noc/differential_dynamic_programming.py: interior_point_ddp, D:189-208):
  * the whole barrier schedule of DDP iterations (second-order backward pass with the Vx . fxx

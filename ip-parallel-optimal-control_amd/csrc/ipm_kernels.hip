@@ -369,7 +369,8 @@ __global__ __launch_bounds__(256) void trial_kernel(noc_family prm, noc_ipm_ws w
     rinc = 2.0;                                           // P:135 / S:111
     // P:243-245; the rollout of the new stage happens in the next step (ROLLOUT_PENDING, see
     // rollout_kernel)
-    phase = (nbp > 1e-4) ? NOC_PHASE_ROLLOUT_PENDING : NOC_PHASE_DONE;
+    // (NOC_WS_ONE_STAGE: newton_oc runs a single barrier stage)
+    phase = (nbp > 1e-4 && !(w.flags & NOC_WS_ONE_STAGE)) ? NOC_PHASE_ROLLOUT_PENDING : NOC_PHASE_DONE;
   } else if (mode == NOC_MODE_PAR) {
     phase = end_iter ? NOC_PHASE_LINEARIZE : NOC_PHASE_SOLVE;
   } else {

@@ -442,6 +442,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       }
     }
     if (capped || !(bp > 1e-4)) break;                          // P:243-245
+    if (w.flags & NOC_WS_ONE_STAGE) break;                      // newton_oc: one stage
   }
   if (l == 0) {
     w.bp[b] = bp;

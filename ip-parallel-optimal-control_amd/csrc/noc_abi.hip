@@ -399,6 +399,66 @@ int noc_ddp_solve(const noc_family* fam, int N, int Bt, const double* x0, double
                                    max_passes, static_cast<hipStream_t>(stream)), "ddp_solve");
 }
 
+int noc_derivatives(const noc_family* fam, int N, int B, const double* x, const double* u,
+                    const double* bp, double* cx, double* cu, double* cxx, double* cuu,
+                    double* cxu, double* fx, double* fu, double* fxx, double* fuu, double* fxu,
+                    void* stream) {
+  if (!fam) return fail(-2, "family is NULL");
+  if (!noc::family_supported(*fam)) return fail(-1, "unsupported problem family (kind/nx/nu)");
+  if (N < 1 || B < 0) return fail(-1, "need N >= 1, B >= 0");
+  const void* req[] = {x, u, bp, cx, cu, cxx, cuu, cxu, fx, fu, fxx, fuu, fxu};
+  for (const void* p : req) {
+    int rc = check_ptr(p, "derivatives argument", true, 8);
+    if (rc) return rc;
+  }
+  if (B == 0) return 0;
+  noc::DerivArgs a{N, B, x, u, bp, cx, cu, cxx, cuu, cxu, fx, fu, fxx, fuu, fxu};
+  return hip_status(noc::derivatives(*fam, a, static_cast<hipStream_t>(stream)), "derivatives");
+}
+
+int noc_final_cost_derivs(const noc_family* fam, int B, const double* xN, double* grad,
+                          double* hess, void* stream) {
+  if (!fam) return fail(-2, "family is NULL");
+  if (!noc::family_supported(*fam)) return fail(-1, "unsupported problem family (kind/nx/nu)");
+  if (B < 0) return fail(-1, "need B >= 0");
+  int rc = 0;
+  if ((rc = check_ptr(xN, "xN", true, 8)) || (rc = check_ptr(grad, "grad", true, 8)) ||
+      (rc = check_ptr(hess, "hess", false, 8)))
+    return rc;
+  if (B == 0) return 0;
+  return hip_status(noc::final_cost_derivs(*fam, B, xN, grad, hess, static_cast<hipStream_t>(stream)),
+                    "final_cost_derivs");
+}
+
+int noc_costates(int nx, int N, int B, const double* lamT, const double* cx, const double* fx,
+                 double* lam, int sequential, void* stream) {
+  if (nx < 1 || nx > 8) return fail(-1, "costates support 1 <= nx <= 8");
+  if (N < 1 || B < 0) return fail(-1, "need N >= 1, B >= 0");
+  int rc = 0;
+  if ((rc = check_ptr(lamT, "lamT", true, 8)) || (rc = check_ptr(cx, "cx", true, 8)) ||
+      (rc = check_ptr(fx, "fx", true, 8)) || (rc = check_ptr(lam, "lam", true, 8)))
+    return rc;
+  if (B == 0) return 0;
+  return hip_status(noc::costates(nx, N, B, lamT, cx, fx, lam, sequential,
+                                  static_cast<hipStream_t>(stream)), "costates");
+}
+
+int noc_lqr_params(int nx, int nu, int N, int B, const double* lam, const double* cu,
+                   const double* cxx, const double* cuu, const double* cxu, const double* fu,
+                   const double* fxx, const double* fuu, const double* fxu, double* ru, double* Q,
+                   double* R, double* M, void* stream) {
+  if (nx < 1 || nx > 8 || nu < 1 || nu > 8) return fail(-1, "lqr_params support nx, nu <= 8");
+  if (N < 1 || B < 0) return fail(-1, "need N >= 1, B >= 0");
+  const void* req[] = {lam, cu, cxx, cuu, cxu, fu, fxx, fuu, fxu, ru, Q, R, M};
+  for (const void* p : req) {
+    int rc = check_ptr(p, "lqr_params argument", true, 8);
+    if (rc) return rc;
+  }
+  if (B == 0) return 0;
+  noc::LqrArgs a{nx, nu, N, B, lam, cu, cxx, cuu, cxu, fu, fxx, fuu, fxu, ru, Q, R, M};
+  return hip_status(noc::lqr_params(a, static_cast<hipStream_t>(stream)), "lqr_params");
+}
+
 static int kkt_and_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* stream) {
   // the trial step needs dx, du only: gains stay on chip when they fit (ws->K, ws->d otherwise)
   const bool on_chip = noc_kkt_gains_on_chip(fam->nx, fam->nu, ws->N, ws->lanes) == 1;

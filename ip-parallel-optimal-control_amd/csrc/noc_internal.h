@@ -40,6 +40,24 @@ inline size_t kkt_lds_bytes_rt(int nx, int nu, int N, int L) {
   return bytes <= 20480 ? bytes : 0;
 }
 
+// standalone building blocks (derivatives.hip)
+struct DerivArgs {
+  int N, B;
+  const double *x, *u, *bp;
+  double *cx, *cu, *cxx, *cuu, *cxu, *fx, *fu, *fxx, *fuu, *fxu;
+};
+struct LqrArgs {
+  int nx, nu, N, B;
+  const double *lam, *cu, *cxx, *cuu, *cxu, *fu, *fxx, *fuu, *fxu;
+  double *ru, *Q, *R, *M;
+};
+hipError_t derivatives(const noc_family& p, const DerivArgs& a, hipStream_t s);
+hipError_t final_cost_derivs(const noc_family& p, int B, const double* xN, double* grad,
+                             double* hess, hipStream_t s);
+hipError_t costates(int nx, int N, int B, const double* lamT, const double* cx, const double* fx,
+                    double* lam, int sequential, hipStream_t s);
+hipError_t lqr_params(const LqrArgs& a, hipStream_t s);
+
 hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t stream);
 // lanes == 1: horizon-sequential solve, one trajectory per nx-lane group (kkt_group_impl.h)
 hipError_t kkt_group_dispatch(int nx, int nu, const KKTArgs& a, hipStream_t stream);

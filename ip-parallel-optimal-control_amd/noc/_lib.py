@@ -51,12 +51,13 @@ class NocFamily(ctypes.Structure):
 
 WS_DOUBLE_FIELDS = ["x", "u", "x0", "A", "B", "Q", "R", "M", "r", "P", "cx", "cu", "lc", "lam",
                     "dx", "du", "pred", "K", "d"]
+WS_ONE_STAGE = 1  # NocIpmWs.flags bit: stop after one barrier stage (newton_oc)
 WS_INT_FIELDS = ["feasible", "phase", "kkt_active", "it", "inner", "total_it", "kkt_solves"]
 WS_STATE_FIELDS = ["bp", "rp", "rinc", "cost", "hu", "gnorm", "reg"]
 
 
 class NocIpmWs(ctypes.Structure):
-    _fields_ = ([("Bt", _i), ("N", _i), ("lanes", _i), ("reserved", _i)]
+    _fields_ = ([("Bt", _i), ("N", _i), ("lanes", _i), ("flags", _i)]
                 + [(f, _dp) for f in WS_DOUBLE_FIELDS]
                 + [(f, _dp) for f in WS_INT_FIELDS] + [(f, _dp) for f in WS_STATE_FIELDS])
 
@@ -75,6 +76,10 @@ SIGNATURES.update({
     "noc_ipm_solve_supported": (_i, [_fp, _i, _i]),
     "noc_debug_phase_cycles": (_i, [ctypes.POINTER(ctypes.c_longlong), _i, _i]),
     "noc_ipm_solve": (_i, [_fp, _wp, _i, _i, ctypes.c_double, _i, _dp]),
+    "noc_derivatives": (_i, [_fp, _i, _i] + [_dp] * 13 + [_dp]),
+    "noc_final_cost_derivs": (_i, [_fp, _i, _dp, _dp, _dp, _dp]),
+    "noc_costates": (_i, [_i, _i, _i, _dp, _dp, _dp, _dp, _i, _dp]),
+    "noc_lqr_params": (_i, [_i] * 4 + [_dp] * 13 + [_dp]),
     "noc_ddp_work_doubles": (ctypes.c_longlong, [_i, _i, _i, _i]),
     "noc_ddp_supported": (_i, [_fp]),
     "noc_ddp_solve": (_i, [_fp, _i, _i] + [_dp] * 6 + [ctypes.c_double, _i, _dp]),

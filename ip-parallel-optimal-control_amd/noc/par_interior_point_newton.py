@@ -1,11 +1,17 @@
 """Parallel-in-time interior-point solver -- drop-in for noc/par_interior_point_newton.py.
 
-`par_interior_point_optimal_control(ocp, controls, initial_state) -> (controls*, iterations)`
-keeps the reference signature (P:228-254).  Differences, all additive:
-  * inputs may carry a leading batch axis (controls (B, N, nu), initial_state (B, nx)); the
-    result is then batched too -- each trajectory follows its own reference control flow;
-  * the whole loop runs on the MI355X (libnoc_hip.so); `ocp.family` must be a registered family
-    (noc.problems) because device code cannot call Python callables;
+Every public function of the reference module is here with its signature (P:13-254):
+compute_derivatives, compute_lqr_params, check_traj_feasibility, noc_to_lqt, par_Newton,
+newton_oc, par_interior_point_optimal_control.  They run on the MI355X: the building blocks as
+batched HIP kernels (noc_derivatives, noc_costates, noc_lqr_params, noc_kkt_solve), the loops as
+the persistent whole-solve kernel (noc_ipm_solve) or the launch-per-phase driver.
+
+Differences, all additive:
+  * inputs may carry a leading batch axis (controls (B, N, nu), initial_state (B, nx), states
+    (B, N+1, nx)); the result is then batched too -- each trajectory follows its own reference
+    control flow (jax.vmap semantics);
+  * `ocp.family` must be a registered family (noc.problems built-ins or noc.families
+    .register_family) because device code cannot call Python callables;
   * `terminal`: "stage0" (default: the reference par path's terminal Hessian XT = Q[0], P:73 --
     what par_Newton actually feeds its LQT) or "final_cost" (hessian(final_cost), the reference
     seq path S:66).  The default reproduces the reference par loop's iteration counts (e.g.
@@ -13,20 +19,128 @@ keeps the reference signature (P:228-254).  Differences, all additive:
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
+import torch
 
 from . import _lib
 from .ipm import BatchedIPM
-from .optimal_control_problem import OCP
+from .optimal_control_problem import OCP, Derivatives
 
 _TERMINAL = {"final_cost": _lib.TERMINAL_FINAL_COST, "stage0": _lib.TERMINAL_STAGE0}
 
 
+def _family(ocp: OCP):
+    if getattr(ocp, "family", None) is None:
+        raise _lib.NocError("OCP has no registered device family (noc.problems / noc.families): "
+                            "the HIP kernels cannot evaluate Python callables")
+    return ocp.family
+
+
+def _dev(t, name="array"):
+    if isinstance(t, torch.Tensor):
+        _lib.require_device(t, name)
+        return t.to(torch.float64).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(t, dtype=np.float64), device="cuda")
+
+
+def compute_derivatives(ocp: OCP, states, controls, bp) -> Derivatives:
+    """P:13-28: per-stage grad / hessian of stage_cost and jacrev / second derivatives of the
+    dynamics at (x_k, u_k), k < N (noc_derivatives).  states (N+1, nx), controls (N, nu) (or
+    batched), bp a scalar or one per trajectory."""
+    fam = _family(ocp)
+    x, u = _dev(states, "states"), _dev(controls, "controls")
+    single = x.dim() == 2
+    if single:
+        x, u = x[None], u[None]
+    B, N, nx, nu = u.shape[0], u.shape[1], fam.nx, fam.nu
+    bpt = torch.as_tensor(bp, dtype=torch.float64, device=x.device).reshape(-1).expand(B).contiguous()
+    f64 = dict(dtype=torch.float64, device=x.device)
+    shapes = dict(cx=(nx,), cu=(nu,), cxx=(nx, nx), cuu=(nu, nu), cxu=(nx, nu), fx=(nx, nx),
+                  fu=(nx, nu), fxx=(nx, nx, nx), fuu=(nx, nu, nu), fxu=(nx, nx, nu))
+    out = {k: torch.empty((B, N) + s, **f64) for k, s in shapes.items()}
+    lib = _lib.load_for(fam)
+    _lib.check(lib.noc_derivatives(ctypes.byref(fam.to_c()), N, B, x.data_ptr(), u.data_ptr(),
+                                   bpt.data_ptr(), *(out[k].data_ptr() for k in Derivatives._fields),
+                                   _lib.stream_handle(x.device)), "noc_derivatives", lib)
+    d = Derivatives(*(out[k] for k in Derivatives._fields))
+    return Derivatives(*(t[0] for t in d)) if single else d
+
+
+def compute_lqr_params(lagrange_multipliers, d: Derivatives):
+    """P:31-42: ru = cu + fu' l, Q = cxx + l.fxx, R = cuu + l.fuu, M = cxu + l.fxu with
+    l = lambda[1:] (noc_lqr_params)."""
+    lam = _dev(lagrange_multipliers, "lagrange_multipliers")
+    dd = Derivatives(*(_dev(t) for t in d))
+    single = lam.dim() == 2
+    if single:
+        lam = lam[None]
+        dd = Derivatives(*(t[None] for t in dd))
+    B, N, nu = dd.cu.shape
+    nx = lam.shape[-1]
+    f64 = dict(dtype=torch.float64, device=lam.device)
+    ru, Q, R, M = (torch.empty(B, N, *s, **f64) for s in ((nu,), (nx, nx), (nu, nu), (nx, nu)))
+    lib = _lib.load()
+    _lib.check(lib.noc_lqr_params(nx, nu, N, B, lam.data_ptr(), *(getattr(dd, k).data_ptr() for k in
+                                  ("cu", "cxx", "cuu", "cxu", "fu", "fxx", "fuu", "fxu")),
+                                  ru.data_ptr(), Q.data_ptr(), R.data_ptr(), M.data_ptr(),
+                                  _lib.stream_handle(lam.device)), "noc_lqr_params", lib)
+    res = (ru, Q, R, M)
+    return tuple(t[0] for t in res) if single else res
+
+
+def check_traj_feasibility(ocp: OCP, x, u):
+    """P:45-47: all(constraints(x_k, u_k) <= 0) -- for the registered families' box constraints
+    |u_j| <= u_bound (none when u_bound <= 0); one flag per trajectory if batched."""
+    fam = _family(ocp)
+    u = _dev(u, "u")
+    if fam.u_bound <= 0:
+        ok = torch.ones(u.shape[:-2], dtype=torch.bool, device=u.device)
+    else:
+        ok = ((u - fam.u_bound <= 0) & (-u - fam.u_bound <= 0)).flatten(-2).all(-1)
+    return ok
+
+
+def noc_to_lqt(ru, Q, R, M, A, B):
+    """P:50-84: the paroc tracking-form LQT of the Newton step (references r, s by the two
+    per-stage solves; terminal XT = Q[0], HT = I, rT = 0).  Needs Q invertible, like the
+    reference; the solvers here never use this form (noc_kkt_solve takes the canonical blocks)."""
+    from .lqt import LQT
+    ru, Q, R, M, A, B = (_dev(t) for t in (ru, Q, R, M, A, B))
+    XinvM = torch.linalg.solve(Q, M)
+    s = -torch.linalg.solve(R - M.transpose(-1, -2) @ XinvM, ru.unsqueeze(-1)).squeeze(-1)
+    r = -(XinvM @ s.unsqueeze(-1)).squeeze(-1)
+    T, nx, nu = Q.shape[-3], Q.shape[-1], R.shape[-1]
+    eye = lambda n: torch.eye(n, dtype=torch.float64, device=Q.device).expand(*Q.shape[:-2], n, n)
+    zeros = torch.zeros(*Q.shape[:-1], dtype=torch.float64, device=Q.device)
+    return LQT(A, B, zeros, Q[..., 0, :, :], torch.eye(nx, dtype=torch.float64, device=Q.device)
+               .expand(*Q.shape[:-3], nx, nx), torch.zeros(*Q.shape[:-3], nx, dtype=torch.float64,
+                                                           device=Q.device),
+               Q, eye(nx), r, R, eye(nu), s, M)
+
+
+def par_Newton(nominal_states, d: Derivatives, reg_param, ru, Q, R, M):
+    """P:107-124: reg = reg_param * ||cu||_F added to R, the LQT's bwd + fwd pass from dx_0 = 0
+    with terminal Hessian XT = Q[0] -> (dx, du, pred_reduction, feasible, ru).  One fused KKT
+    launch (noc_kkt_solve) instead of noc_to_lqt + par_bwd_pass + par_fwd_pass."""
+    from . import lqt
+    ru, Q, R, M = (_dev(t) for t in (ru, Q, R, M))
+    fx, fu, cu = _dev(d.fx), _dev(d.fu), _dev(d.cu)
+    single = Q.dim() == 3
+    if single:
+        ru, Q, R, M, fx, fu, cu = (t[None] for t in (ru, Q, R, M, fx, fu, cu))
+    gnorm = torch.linalg.vector_norm(cu.flatten(1), dim=1)
+    reg = (torch.as_tensor(reg_param, dtype=torch.float64, device=Q.device).reshape(-1) * gnorm)
+    P = Q[:, 0].contiguous()
+    out = lqt.kkt_solve(fx, fu, Q, R, M, ru, P, reg=reg.contiguous(), want_gains=False)
+    res = (out.dx, out.du, out.pred, out.feasible.bool(), ru)
+    return tuple(t[0] for t in res) if single else res
+
+
 def _run(ocp: OCP, controls, initial_state, mode, terminal="stage0", lanes=0,
-         device="cuda", return_info=False):
-    if ocp.family is None:
-        raise _lib.NocError("OCP has no registered device family (use noc.problems.*): the HIP "
-                            "kernels cannot evaluate Python callables")
+         device="cuda", return_info=False, one_stage_bp=None):
+    fam = _family(ocp)
     u = np.asarray(controls, dtype=np.float64)
     x0 = np.asarray(initial_state, dtype=np.float64)
     single = u.ndim == 2
@@ -35,17 +149,29 @@ def _run(ocp: OCP, controls, initial_state, mode, terminal="stage0", lanes=0,
     Bt, N, _ = u.shape
     from .ipm import persistent_supported
     # whole solve in one launch when the family / horizon allows it (same results, lanes 64)
-    persistent = lanes in (0, 64) and persistent_supported(ocp.family, N)
-    eng = BatchedIPM(ocp.family, N, Bt, device=device, lanes=lanes, persistent=persistent)
+    persistent = lanes in (0, 64) and persistent_supported(fam, N)
+    eng = BatchedIPM(fam, N, Bt, device=device, lanes=lanes, persistent=persistent)
+    if one_stage_bp is not None:
+        eng.ws.flags |= _lib.WS_ONE_STAGE
     eng.load(u, x0)
-    steps = eng.solve(mode=mode, terminal=_TERMINAL[terminal])
+    bp0 = 0.1 if one_stage_bp is None else float(one_stage_bp)
+    steps = eng.solve(mode=mode, terminal=_TERMINAL[terminal], bp0=bp0)
     U, iters, solves = eng.result()
+    X = eng.t["x"].cpu().numpy()
     U, iters, solves = U.cpu().numpy(), iters.cpu().numpy(), solves.cpu().numpy()
     if single:
-        U, iters, solves = U[0], int(iters[0]), int(solves[0])
+        U, iters, solves, X = U[0], int(iters[0]), int(solves[0]), X[0]
+    if one_stage_bp is not None:
+        return X, U, iters
     if return_info:
         return U, iters, dict(kkt_solves=solves, device_steps=steps)
     return U, iters
+
+
+def newton_oc(ocp: OCP, controls, initial_state, barrier_param, terminal="stage0"):
+    """P:127-225: ONE barrier stage -- rollout, then Newton iterations with the retry loop until
+    |Hu|inf < 1e-4 (or 1000 iterations) -> (states, controls, iterations)."""
+    return _run(ocp, controls, initial_state, _lib.MODE_PAR, terminal, one_stage_bp=barrier_param)
 
 
 def par_interior_point_optimal_control(ocp: OCP, controls, initial_state, terminal="stage0",

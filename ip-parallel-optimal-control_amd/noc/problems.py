@@ -87,6 +87,11 @@ def _quadratic_barrier_costs(fam: Family):
     def total_cost(states, controls, bp):
         return final_cost(states[-1]) + sum(stage_cost(x, u, bp) for x, u in zip(states[:-1], controls))
 
+    # the device solvers find the family through the callables too (seq bwd_pass takes
+    # ocp.final_cost, S:42-66)
+    for fn in (final_cost, stage_cost, total_cost):
+        fn.family = fam
+
     constraints = cons if fam.u_bound > 0 else (lambda state, control: -1.0)
     return constraints, stage_cost, final_cost, total_cost
 
