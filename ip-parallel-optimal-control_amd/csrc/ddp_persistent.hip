@@ -29,6 +29,12 @@
 
 namespace noc {
 
+// Diagnostic per-pass trace of the DDP decisions (tools/ddp_trace_diff.py), set by the debug
+// export noc_debug_set_ddp_trace (not part of the ABI header); NULL in product use.
+__device__ double* g_ddp_trace = nullptr;
+__device__ int g_ddp_trace_cap = 0;
+__device__ int g_ddp_trace_traj = 0;
+
 struct DdpArgs {
   int N, Bt, max_passes;
   double bp0;
@@ -279,6 +285,12 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
         r_inc = success ? 2.0 : 2.0 * r_inc;                        // D:133
         rp = fmin(fmax(rp, 1e-16), 1e16);                           // D:135
         inner += 1;
+        if (g_ddp_trace && lead && b < g_ddp_trace_traj && passes <= g_ddp_trace_cap) {
+          // diagnostic trace (noc_debug_set_ddp_trace; off in product use): one record per pass
+          double* tr = g_ddp_trace + ((size_t)b * g_ddp_trace_cap + (passes - 1)) * 10;
+          tr[0] = bp; tr[1] = it; tr[2] = inner; tr[3] = pred; tr[4] = gain;
+          tr[5] = success ? 1.0 : 0.0; tr[6] = rp; tr[7] = hn; tr[8] = cost; tr[9] = new_cost;
+        }
         if (passes >= a.max_passes) capped = true;
         if (success || inner > 500 || capped) break;                // D:147-152
       }
@@ -353,3 +365,12 @@ hipError_t ddp_solve(const noc_family& p, int N, int Bt, const double* x0, doubl
 }
 
 }  // namespace noc
+
+// debug export: trace buffer of traj x cap x 10 doubles (bp, it, inner, pred, gain, success, rp,
+// |Hu|, cost, new_cost per backward pass) for the first `traj` trajectories; buf = NULL disables
+extern "C" int noc_debug_set_ddp_trace(double* buf, int cap, int traj) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(noc::g_ddp_trace), &buf, sizeof(buf)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(noc::g_ddp_trace_cap), &cap, sizeof(cap)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(noc::g_ddp_trace_traj), &traj, sizeof(traj)) != hipSuccess) return -1;
+  return 0;
+}
