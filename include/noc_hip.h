@@ -192,14 +192,19 @@ int noc_ipm_promote(const noc_ipm_ws* ws, void* stream);
 /* Persistent solve: the WHOLE barrier schedule (rollout, Newton / retry loops, barrier updates)
  * of every trajectory in ONE launch, one wave64 per trajectory running its own reference control
  * flow back to back (no per-step launches, no host polls, no lockstep across trajectories).
- * Same arithmetic and results as the noc_ipm_init + noc_ipm_step loop at lanes = 64.  Requires
+ * Same arithmetic and results as the noc_ipm_init + noc_ipm_step loop at lanes = 64 -- except that
+ * a batch of at most one trajectory per CU runs the wide kernel (four waves per trajectory, blocks
+ * in LDS; same control flow, the scans associate differently, so iterates agree to fp64 rounding,
+ * not bitwise); the environment variable NOC_PERSIST_WIDE=0 forces the one-wave kernel.  Requires
  * ws->lanes == 64 and a KKT step that fits in LDS (noc_ipm_solve_supported).  A trajectory that
  * reaches max_solves KKT solves stops with phase != NOC_PHASE_DONE.  On return (stream order)
  * u, x, bp, rp, r_inc, cost, hu, it, total_it, kkt_solves and phase hold the final state. */
 int noc_ipm_solve_supported(const noc_family* fam, int N, int lanes);
 /* Timing-only: per-phase cycle counters of the persistent solver's workgroup 0 (rollout,
- * linearise, costate + blocks, KKT scan, trial, Newton iterations); all zero unless the library
- * was built with -DNOC_PERSIST_PROFILE.  reset != 0 zeroes them after reading.  Synchronous. */
+ * linearise, costate + blocks, KKT scan, trial, Newton iterations; n up to 16: slots 8..14 split
+ * the wide kernel's KKT solve into prepend, in-wave scan, cross-wave join, Riccati, pred
+ * reduction, forward scan, propagate); all zero unless the library was built with
+ * -DNOC_PERSIST_PROFILE.  reset != 0 zeroes them after reading.  Synchronous. */
 int noc_debug_phase_cycles(long long* out, int n, int reset);
 int noc_ipm_solve(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, double bp0,
                   int max_solves, void* stream);

@@ -507,7 +507,9 @@ static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, in
 int debug_phase_cycles(long long* out, int n, int reset) {
   long long host[8];
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase_cycles), sizeof(host)) != hipSuccess) return -1;
-  for (int i = 0; i < n && i < 8; ++i) out[i] = host[i];
+  long long wide[16];
+  if (debug_wide_cycles(wide, 16, reset) != 0) return -1;  // the wide kernel's (ipm_wide.hip)
+  for (int i = 0; i < n && i < 16; ++i) out[i] = (i < 8 ? host[i] : 0) + wide[i];
   if (reset) {
     const long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), zero, sizeof(zero)) != hipSuccess) return -1;
@@ -537,8 +539,20 @@ static hipError_t solve_family(const noc_family& p, const noc_ipm_ws& w, int mod
   else return hipErrorInvalidValue;
 }
 
+// The wide kernel (ipm_wide.hip: 4 waves and the LDS of one CU per trajectory) when the batch
+// leaves CUs idle anyway (B <= #CUs: the reference's B = 1 runs); NOC_PERSIST_WIDE=0|1 overrides.
+static bool use_wide(const noc_family& p, const noc_ipm_ws& w) {
+  const char* env = getenv("NOC_PERSIST_WIDE");
+  if (env && atoi(env) == 0) return false;
+  if (!ipm_wide_supported(p, w.N)) return false;
+  if (env && atoi(env) == 1) return true;
+  static const int cus = device_simds() / 4;
+  return cus > 0 && w.Bt <= cus;
+}
+
 hipError_t ipm_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal, double bp0,
                      int max_solves, hipStream_t s) {
+  if (use_wide(p, w)) return ipm_solve_wide(p, w, mode, terminal, bp0, max_solves, s);
 #define NOC_FAMILY(K, X, U)                                                              \
   if (p.kind == K && p.nx == X && p.nu == U)                                             \
     return solve_family<K, X, U>(p, w, mode, terminal, bp0, max_solves, s);

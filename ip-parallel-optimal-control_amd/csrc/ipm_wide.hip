@@ -1,0 +1,807 @@
+// Wide persistent interior-point solver: the whole barrier schedule of ONE trajectory per
+// W-wave workgroup (W = 4: 256 lanes), the trajectory's LQ blocks, states, controls and step held
+// in LDS for the whole solve (fp64, gfx950).
+//
+// Same reference control flow as ipm_persistent.hip (par_interior_point_optimal_control /
+// newton_oc, noc/par_interior_point_newton.py:127-254; seq S:108-202), for the regime where the
+// batch does not fill the chip -- the reference's own B = 1 timing runs and the stragglers of a
+// large batch -- where a trajectory's latency is the wall time:
+//   * the stage-parallel work (linearise P:13-28, the costate sweep C:34-54 fused with the LQ
+//     blocks P:31-42, the trial point P:156-175) is spread over 64 W lanes: one stage per lane up
+//     to N = 64 W instead of N / 64;
+//   * the KKT scan (par_Newton, P:107-124) keeps the in-wave reverse Hillis-Steele of the 64-lane
+//     scan (kkt_scan_impl.h: chunk element by Riccati-form prepend, combine_shfl) and joins the
+//     W waves through LDS with value-only applications of the later waves' aggregates, so the
+//     dependent chain stays at six combine levels while each lane's chunk shrinks to one stage;
+//     the forward affine scan is joined the same way;
+//   * nothing goes through HBM between the phases (linearise -> costates -> LQ
+//     blocks -> KKT solve -> trial in one launch, blocks resident in LDS).
+// Layouts in LDS are field-major ([element][stage]) so that lanes holding consecutive stages
+// touch consecutive words.  One workgroup per CU (the LDS image is up to ~150 KB).
+#include <hip/hip_runtime.h>
+#include <cstdlib>
+
+#include "../../include/noc_hip.h"
+#include "ipm_family.h"
+#include "kkt_scan_impl.h"
+#include "noc_internal.h"
+
+namespace noc {
+
+// Per-phase cycle counters of workgroup 0 (timing-only, -DNOC_PERSIST_PROFILE builds; summed into
+// noc_debug_phase_cycles with the one-wave kernel's): rollout, linearise, costate + blocks, KKT
+// scan, trial, number of Newton iterations.
+__device__ long long g_wide_cycles[16];
+#ifdef NOC_PERSIST_PROFILE
+#define NOC_WPHASE(i) do { const long long t_ = clock64(); if (b == 0 && t == 0) g_wide_cycles[i] += t_ - t_prev; t_prev = t_; } while (0)
+// sub-phases of the KKT solve (slots 8..15), timed by wave 0 lane 0 without moving t_prev
+#define NOC_WSUB(i) do { const long long t_ = clock64(); if (b == 0 && t == 0) g_wide_cycles[8 + (i)] += t_ - t_sub; t_sub = t_; } while (0)
+#else
+#define NOC_WPHASE(i) do { } while (0)
+#define NOC_WSUB(i) do { } while (0)
+#endif
+
+namespace {
+
+constexpr int kWideWaves = 4;
+
+// LDS image of one trajectory (offsets in doubles)
+template <int NX, int NU>
+struct WideLds {
+  static constexpr int KD = NU * (NX + 1);
+  static constexpr int SQ = Sym<NX>::SZ, SR = Sym<NU>::SZ;
+  int x, u, A, B, Q, R, M, r, cx, cu, lc, kd, agg, red, P, total;
+  __host__ __device__ WideLds(int N, int W) {
+    int o = 0;
+    x = o; o += (N + 1) * NX;
+    u = o; o += N * NU;
+    A = o; o += NX * NX * N;
+    B = o; o += NX * NU * N;
+    Q = o; o += SQ * N;
+    R = o; o += SR * N;
+    M = o; o += NX * NU * N;
+    r = o; o += NU * N;
+    cx = o; o += NX * N;
+    cu = o; o += NU * N;
+    lc = o; o += N;
+    kd = o; o += KD * (N + 1);  // K, d per stage; then dx [i][0..N], du [NX + j][0..N-1]
+    agg = o; o += W * 64;       // per-wave aggregates (scan elements / affine maps)
+    red = o; o += W * 8;        // per-wave partial reductions
+    P = o; o += NX * NX;        // terminal Hessian
+    total = o;
+  }
+};
+
+template <int E>
+NOC_DEV void fget(const double* base, int N, int s, double* v) {
+  NOC_UNROLL for (int e = 0; e < E; ++e) v[e] = base[(size_t)e * N + s];
+}
+template <int E>
+NOC_DEV void fput(double* base, int N, int s, const double* v) {
+  NOC_UNROLL for (int e = 0; e < E; ++e) base[(size_t)e * N + s] = v[e];
+}
+
+// e1 <- e1 (x) (value-only e2 = (J2, nu2)): the true value function at e1's start given the value
+// at its end (the VALUE_ONLY branch of combine_shfl with the partner given explicitly)
+template <int NX>
+NOC_DEV void apply_value(Elem<NX>& e1, const Sym<NX>& J2, const Vec<NX>& nu2) {
+  double X[NX][NX], Y[NX][NX];
+  auto build = [&]() {
+    NOC_UNROLL for (int i = 0; i < NX; ++i)
+      NOC_UNROLL for (int j = 0; j < NX; ++j) {
+        double s = (i == j) ? 1.0 : 0.0;
+        NOC_UNROLL for (int k = 0; k < NX; ++k) s += e1.C(i, k) * J2(k, j);
+        X[i][j] = s;
+        Y[i][j] = e1.A(i, j);
+      }
+  };
+  build();
+  Mat<NX, NX> J2A1;
+  Vec<NX> w;
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    double sw = nu2[i];
+    NOC_UNROLL for (int k = 0; k < NX; ++k) sw += J2(i, k) * e1.b[k];
+    w[i] = sw;
+    NOC_UNROLL for (int j = 0; j < NX; ++j) {
+      double s = 0.0;
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += J2(i, k) * e1.A(k, j);
+      J2A1(i, j) = s;
+    }
+  }
+  // every lane of the workgroup takes the same branch only within a wave: the fallback is
+  // per-lane (no shuffles here), so no uniformity is needed
+  if (!lu_np_solve<NX, NX>(X, Y)) {
+    build();
+    lu_pp_solve<NX, NX>(X, Y);
+  }
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    NOC_UNROLL for (int j = i; j < NX; ++j) {
+      double s = e1.J(i, j);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * J2A1(k, j);
+      e1.J(i, j) = s;
+    }
+    double s = e1.nu[i];
+    NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * w[k];
+    e1.nu[i] = s;
+  }
+  set_zero(e1.A);
+  set_zero(e1.b);
+  set_zero(e1.C);
+}
+
+template <int NX>
+NOC_DEV void elem_put(double* p, const Elem<NX>& e) {
+  int o = 0;
+  NOC_UNROLL for (int i = 0; i < NX * NX; ++i) p[o++] = e.A.v[i];
+  NOC_UNROLL for (int i = 0; i < NX; ++i) p[o++] = e.b.v[i];
+  NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) p[o++] = e.C.v[i];
+  NOC_UNROLL for (int i = 0; i < NX; ++i) p[o++] = e.nu.v[i];
+  NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) p[o++] = e.J.v[i];
+}
+template <int NX>
+NOC_DEV void elem_get(const double* p, Elem<NX>& e) {
+  int o = 0;
+  NOC_UNROLL for (int i = 0; i < NX * NX; ++i) e.A.v[i] = p[o++];
+  NOC_UNROLL for (int i = 0; i < NX; ++i) e.b.v[i] = p[o++];
+  NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) e.C.v[i] = p[o++];
+  NOC_UNROLL for (int i = 0; i < NX; ++i) e.nu.v[i] = p[o++];
+  NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) e.J.v[i] = p[o++];
+}
+
+}  // namespace
+
+// W waves per trajectory (blockDim = 64 W), one workgroup per trajectory.
+template <int KIND, int NX, int NU, int W>
+__global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc_ipm_ws w, int mode,
+                                                             int terminal, double bp0,
+                                                             int max_solves) {
+  constexpr int T = 64 * W;
+  constexpr int KD = NU * (NX + 1);
+  constexpr int ESZ = NX * NX + 2 * NX + 2 * Sym<NX>::SZ;  // scan element in doubles
+  static_assert(ESZ <= 64 && NX * NX + NX <= 64, "aggregate slot");
+  extern __shared__ __attribute__((aligned(16))) double noc_smem[];
+  const int b = blockIdx.x;
+  const int t = threadIdx.x, wv = t >> 6, l = t & 63;
+  if (b >= w.Bt) return;  // uniform over the workgroup
+  Fam<KIND, NX, NU> f(prm);
+  const int N = w.N;
+  const WideLds<NX, NU> L(N, W);
+  double* sx = noc_smem + L.x;
+  double* su = noc_smem + L.u;
+  double* sA = noc_smem + L.A;
+  double* sB = noc_smem + L.B;
+  double* sQ = noc_smem + L.Q;
+  double* sR = noc_smem + L.R;
+  double* sM = noc_smem + L.M;
+  double* sr = noc_smem + L.r;
+  double* scx = noc_smem + L.cx;
+  double* scu = noc_smem + L.cu;
+  double* slc = noc_smem + L.lc;
+  double* skd = noc_smem + L.kd;
+  double* sagg = noc_smem + L.agg;
+  double* sred = noc_smem + L.red;
+  double* sP = noc_smem + L.P;
+  const Chunks ch(N, T);
+  const int start = ch.start(t), len = ch.len(t);
+  const bool last = (t == T - 1);
+  double* Xg = w.x + (size_t)b * (N + 1) * NX;
+  double* Ug = w.u + (size_t)b * N * NU;
+  // dx, du live in the K/d region once the forward pass has consumed the gains
+  auto dxs = [&](int i, int s) -> double& { return skd[(size_t)i * (N + 1) + s]; };
+  auto dus = [&](int j, int s) -> double& { return skd[(size_t)(NX + j) * (N + 1) + s]; };
+  auto kds = [&](int i, int s) -> double& { return skd[(size_t)i * (N + 1) + s]; };
+
+  // workgroup reductions of up to 4 doubles (sum / nan-propagating max), every thread gets the
+  // result, combined in wave order (deterministic)
+  auto wg_reduce = [&](double* v, int n, const bool* is_max) {
+    NOC_UNROLL for (int k = 0; k < 4; ++k) {
+      if (k < n) {
+        NOC_UNROLL for (int off = 32; off > 0; off >>= 1) {
+          const double o = __shfl_xor(v[k], off, 64);
+          v[k] = is_max[k] ? nan_max(v[k], o) : v[k] + o;
+        }
+      }
+    }
+    __syncthreads();
+    if (l == 0) NOC_UNROLL for (int k = 0; k < 4; ++k) if (k < n) sred[wv * 8 + k] = v[k];
+    __syncthreads();
+    NOC_UNROLL for (int k = 0; k < 4; ++k) {
+      if (k < n) {
+        double a = sred[k];
+        for (int q = 1; q < W; ++q) a = is_max[k] ? nan_max(a, sred[q * 8 + k]) : a + sred[q * 8 + k];
+        v[k] = a;
+      }
+    }
+  };
+
+  // controls in
+  for (int i = t; i < N * NU; i += T) su[(i % NU) * N + i / NU] = Ug[i];
+  __syncthreads();
+
+  double bp = bp0, rp = 1.0, rinc = 2.0, cost = 0.0, hu = 1.0, gnorm = 0.0;
+  int it = 0, inner = 0, total_it = 0, solves = 0;
+  bool capped = false;
+#ifdef NOC_PERSIST_PROFILE
+  long long t_prev = clock64();
+#endif
+
+  for (;;) {  // ---------------- barrier stages (P:228-254) ----------------
+    // rollout (U:57-63, P:133): wave 0 runs the recurrence, lane (k mod 64) keeps stage k
+    if (wv == 0) {
+      double x[NX];
+      NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = w.x0[(size_t)b * NX + i];
+      if (l < NX) sx[l] = x[l];
+      for (int k = 0; k < N; ++k) {
+        double uk[NU], xn[NX];
+        NOC_UNROLL for (int j = 0; j < NU; ++j) uk[j] = su[(size_t)j * N + k];
+        f.step(x, uk, xn);
+        NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = xn[i];
+        if (l == (k & 63)) NOC_UNROLL for (int i = 0; i < NX; ++i) sx[(size_t)(k + 1) * NX + i] = xn[i];
+      }
+    }
+    __syncthreads();
+    NOC_WPHASE(0);
+    bool relinearize = true, stage_done = false;
+    while (!stage_done) {  // ---------------- Newton iterations (P:127-225) ----------------
+      if (relinearize) {
+        // linearise the own stages (P:13-28)
+        for (int s = start; s < start + len; ++s) {
+          double x[NX], u[NU], fx[NX * NX], fu[NX * NU], cx[NX], cu[NU];
+          NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = sx[(size_t)s * NX + i];
+          NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = su[(size_t)j * N + s];
+          f.jac(x, u, fx, fu);
+          f.stage_grad(x, u, bp, cx, cu);
+          fput<NX * NX>(sA, N, s, fx);
+          fput<NX * NU>(sB, N, s, fu);
+          fput<NX>(scx, N, s, cx);
+          fput<NU>(scu, N, s, cu);
+          slc[s] = f.stage_cost(x, u, bp);
+        }
+        NOC_WPHASE(1);
+        // costates (C:34-54): chunk map lambda_start = G lambda_end + g, in-wave reverse scan,
+        // the waves joined through LDS, then the sweep fused with the LQ blocks (P:31-42)
+        const double* xN = sx + (size_t)N * NX;
+        double lamN[NX];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) lamN[i] = prm.wf[i] * f.err(xN, i);
+        Mat<NX, NX> G;
+        Vec<NX> g;
+        set_identity(G);
+        set_zero(g);
+        for (int s = start + len - 1; s >= start; --s) {
+          double A[NX * NX], cx[NX];
+          fget<NX * NX>(sA, N, s, A);
+          fget<NX>(scx, N, s, cx);
+          Mat<NX, NX> Gn;
+          Vec<NX> gn;
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            double a = cx[i];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) a += A[m * NX + i] * g[m];
+            gn[i] = a;
+            NOC_UNROLL for (int j = 0; j < NX; ++j) {
+              double c = 0.0;
+              NOC_UNROLL for (int m = 0; m < NX; ++m) c += A[m * NX + i] * G(m, j);
+              Gn(i, j) = c;
+            }
+          }
+          G = Gn;
+          g = gn;
+        }
+        if (last) {
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            double a = g[i];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) a += G(i, m) * lamN[m];
+            g[i] = a;
+          }
+          set_zero(G);
+        }
+#pragma unroll 1
+        for (int d = 1; d < 64; d <<= 1) {
+          Mat<NX, NX> G2;
+          Vec<NX> g2;
+          shfl_down_arr<NX * NX>(G.v, G2.v, d, 64);
+          shfl_down_arr<NX>(g.v, g2.v, d, 64);
+          if (l + d >= 64) {  // no partner in this wave: compose with the identity map
+            set_identity(G2);
+            set_zero(g2);
+          }
+          Mat<NX, NX> Gn;
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            double a = g[i];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) a += G(i, m) * g2[m];
+            g[i] = a;
+            NOC_UNROLL for (int j = 0; j < NX; ++j) {
+              double c = 0.0;
+              NOC_UNROLL for (int m = 0; m < NX; ++m) c += G(i, m) * G2(m, j);
+              Gn(i, j) = c;
+            }
+          }
+          G = Gn;
+        }
+        // wave aggregates (lane 0: the map over the whole wave) -> LDS
+        if (l == 0) {
+          NOC_UNROLL for (int i = 0; i < NX * NX; ++i) sagg[wv * 64 + i] = G.v[i];
+          NOC_UNROLL for (int i = 0; i < NX; ++i) sagg[wv * 64 + NX * NX + i] = g[i];
+        }
+        __syncthreads();
+        // costate at the end of this wave's span: the last wave's map is constant, earlier ones
+        // compose the later waves' maps
+        double lw[NX];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) lw[i] = (wv == W - 1) ? lamN[i] : sagg[(W - 1) * 64 + NX * NX + i];
+        for (int q = W - 2; q > wv; --q) {
+          double ln[NX];
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            double a = sagg[q * 64 + NX * NX + i];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) a += sagg[q * 64 + i * NX + m] * lw[m];
+            ln[i] = a;
+          }
+          NOC_UNROLL for (int i = 0; i < NX; ++i) lw[i] = ln[i];
+        }
+        // this lane's chunk-end costate: lane l+1's in-wave map applied to lw (lane 63: lw)
+        Mat<NX, NX> Gd;
+        Vec<NX> gd;
+        shfl_down_arr<NX * NX>(G.v, Gd.v, 1, 64);
+        shfl_down_arr<NX>(g.v, gd.v, 1, 64);
+        double lam[NX];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) {
+          double a = gd[i];
+          NOC_UNROLL for (int m = 0; m < NX; ++m) a += Gd(i, m) * lw[m];
+          lam[i] = (l == 63) ? lw[i] : a;
+        }
+        double red[4] = {0.0, 0.0, 0.0, 0.0};  // cost, max|Hu|, ||cu||^2
+        for (int s = start + len - 1; s >= start; --s) {
+          double x[NX], u[NU], A[NX * NX], Bm[NX * NU], cx[NX], cu[NU];
+          NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = sx[(size_t)s * NX + i];
+          NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = su[(size_t)j * N + s];
+          fget<NX * NX>(sA, N, s, A);
+          fget<NX * NU>(sB, N, s, Bm);
+          fget<NX>(scx, N, s, cx);
+          fget<NU>(scu, N, s, cu);
+          // Q = cxx + l.fxx, R = cuu + l.fuu, M = cxu + l.fxu at l = lambda_{s+1} (P:35-37)
+          double Qf[NX * NX], Rf[NU * NU], M[NX * NU], rr[NU];
+          NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) Qf[i * NX + j] = (i == j) ? prm.wx[i] : 0.0;
+          NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int j = 0; j < NU; ++j) Rf[i * NU + j] = (i == j) ? f.stage_cuu(u, bp, i) : 0.0;
+          NOC_UNROLL for (int i = 0; i < NX * NU; ++i) M[i] = 0.0;
+          f.add_hess_l(x, u, lam, Qf, Rf, M);
+          Sym<NX> Qs;
+          Sym<NU> Rs;
+          NOC_UNROLL for (int i = 0; i < NX; ++i)
+            NOC_UNROLL for (int j = i; j < NX; ++j) Qs(i, j) = (i == j) ? Qf[i * NX + i] : 0.5 * (Qf[i * NX + j] + Qf[j * NX + i]);
+          NOC_UNROLL for (int i = 0; i < NU; ++i)
+            NOC_UNROLL for (int j = i; j < NU; ++j) Rs(i, j) = (i == j) ? Rf[i * NU + i] : 0.5 * (Rf[i * NU + j] + Rf[j * NU + i]);
+          NOC_UNROLL for (int j = 0; j < NU; ++j) {  // ru = cu + fu' lambda_{s+1} (P:34)
+            double a = cu[j];
+            NOC_UNROLL for (int i = 0; i < NX; ++i) a += Bm[i * NU + j] * lam[i];
+            rr[j] = a;
+            red[1] = nan_max(red[1], fabs(a));
+            red[2] += cu[j] * cu[j];
+          }
+          fput<Sym<NX>::SZ>(sQ, N, s, Qs.v);
+          fput<Sym<NU>::SZ>(sR, N, s, Rs.v);
+          fput<NX * NU>(sM, N, s, M);
+          fput<NU>(sr, N, s, rr);
+          if (terminal == NOC_TERMINAL_STAGE0 && s == 0)  // XT = Q[0] (P:73)
+            NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) sP[i * NX + j] = Qs(i, j);
+          double ln[NX];  // lambda_s = cx_s + fx_s' lambda_{s+1}
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            double a = cx[i];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) a += A[m * NX + i] * lam[m];
+            ln[i] = a;
+          }
+          NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = ln[i];
+          red[0] += slc[s];
+        }
+        if (terminal == NOC_TERMINAL_FINAL_COST && last)  // hessian(final_cost) (S:66)
+          NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) sP[i * NX + j] = (i == j) ? prm.wf[i] : 0.0;
+        const bool is_max[4] = {false, true, false, false};
+        wg_reduce(red, 3, is_max);
+        cost = red[0] + f.final_cost(xN);  // total_cost(x, u, bp) (P:142)
+        hu = red[1];                       // max |Hu| (P:158)
+        gnorm = sqrt(red[2]);              // ||cu||_F (P:116)
+        inner = 0;
+        relinearize = false;
+      }
+      const double reg = (mode == NOC_MODE_PAR) ? rp * gnorm : rp;  // P:116-118 / S:51
+      __syncthreads();  // blocks and the terminal Hessian complete before the scan reads them
+      NOC_WPHASE(2);
+#ifdef NOC_PERSIST_PROFILE
+      long long t_sub = clock64();
+#endif
+
+      // ---------------- KKT solve (par_Newton, P:107-124) ----------------
+      // phase 1: this lane's chunk element (Riccati-form prepend, kkt_scan_impl.h)
+      auto stage_from_lds = [&](int s, StageData<NX, NU>& st) {
+        fget<NX * NX>(sA, N, s, st.A.v);
+        fget<NX * NU>(sB, N, s, st.B.v);
+        fget<Sym<NX>::SZ>(sQ, N, s, st.Q.v);
+        fget<Sym<NU>::SZ>(sR, N, s, st.R.v);
+        fget<NX * NU>(sM, N, s, st.M.v);
+        fget<NU>(sr, N, s, st.r.v);
+      };
+      Sym<NX> Pt;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = i; j < NX; ++j) Pt(i, j) = (i == j) ? sP[i * NX + i] : 0.5 * (sP[i * NX + j] + sP[j * NX + i]);
+      Elem<NX> e;
+      set_zero(e.b);
+      set_zero(e.C);
+      set_zero(e.nu);
+      if (last) { set_zero(e.A); e.J = Pt; } else { set_identity(e.A); set_zero(e.J); }
+      for (int s = start + len - 1; s >= start; --s) {
+        StageData<NX, NU> st;
+        stage_from_lds(s, st);
+        prepend<NX, NU, false>(e, st, reg);
+      }
+      NOC_WSUB(0);
+      // phase 2: in-wave reverse Hillis-Steele (the last wave's elements end at the terminal
+      // cost, so its last level is value-only), then the waves joined through LDS
+#pragma unroll 1
+      for (int d = 1; d < 32; d <<= 1) combine_shfl<NX, false, true>(e, d, 64);
+      if (wv == W - 1) combine_shfl<NX, true, true>(e, 32, 64);  // wave-uniform branch
+      else combine_shfl<NX, false, true>(e, 32, 64);
+      NOC_WSUB(1);
+      __syncthreads();  // the aggregate slots were last read by the costate phase
+      if (l == 0) elem_put<NX>(sagg + wv * 64, e);
+      __syncthreads();
+      // value at the start of the next wave's span: later aggregates applied from the end
+      Sym<NX> Jw;
+      Vec<NX> nw;
+      set_zero(Jw);
+      set_zero(nw);
+      if (wv < W - 1) {
+        Elem<NX> ag;
+        elem_get<NX>(sagg + (W - 1) * 64, ag);  // value-only (ends at the terminal cost)
+        Jw = ag.J;
+        nw = ag.nu;
+        for (int q = W - 2; q > wv; --q) {
+          elem_get<NX>(sagg + q * 64, ag);
+          apply_value<NX>(ag, Jw, nw);
+          Jw = ag.J;
+          nw = ag.nu;
+        }
+        apply_value<NX>(e, Jw, nw);  // this lane's true value at its chunk start
+      }
+      NOC_WSUB(2);
+      // phase 3: in-chunk Riccati from the true value at the chunk end (lane l+1's start value;
+      // lane 63: the next wave's; the horizon's last lane: the terminal cost)
+      Sym<NX> S;
+      Vec<NX> v;
+      shfl_down_arr<Sym<NX>::SZ>(e.J.v, S.v, 1, 64);
+      shfl_down_arr<NX>(e.nu.v, v.v, 1, 64);
+      if (l == 63) { S = Jw; v = nw; }
+      if (last) { S = Pt; set_zero(v); }
+      Mat<NX, NX> Phi;
+      Vec<NX> phi;
+      set_identity(Phi);
+      set_zero(phi);
+      double kred[4] = {0.0, 1.0, 0.0, 0.0};  // pred, feasible (as a min), unused
+      for (int s = start + len - 1; s >= start; --s) {
+        StageData<NX, NU> st;
+        stage_from_lds(s, st);
+        Mat<NX, NX> SA;
+        Mat<NX, NU> SB;
+        NOC_UNROLL for (int i = 0; i < NX; ++i) {
+          NOC_UNROLL for (int j = 0; j < NX; ++j) {
+            double a = 0.0;
+            NOC_UNROLL for (int k = 0; k < NX; ++k) a += S(i, k) * st.A(k, j);
+            SA(i, j) = a;
+          }
+          NOC_UNROLL for (int j = 0; j < NU; ++j) {
+            double a = 0.0;
+            NOC_UNROLL for (int k = 0; k < NX; ++k) a += S(i, k) * st.B(k, j);
+            SB(i, j) = a;
+          }
+        }
+        Sym<NU> Quu;
+        NOC_UNROLL for (int i = 0; i < NU; ++i)
+          NOC_UNROLL for (int j = i; j < NU; ++j) {
+            double a = (i == j) ? st.R(i, j) + reg : st.R(i, j);
+            NOC_UNROLL for (int k = 0; k < NX; ++k) a += st.B(k, i) * SB(k, j);
+            Quu(i, j) = a;
+          }
+        double Y[NU][NX + 1];
+        Mat<NU, NX> Qux;
+        Vec<NU> Qu;
+        NOC_UNROLL for (int i = 0; i < NU; ++i) {
+          NOC_UNROLL for (int j = 0; j < NX; ++j) {
+            double a = st.M(j, i);
+            NOC_UNROLL for (int k = 0; k < NX; ++k) a += SB(k, i) * st.A(k, j);
+            Qux(i, j) = a;
+            Y[i][j] = a;
+          }
+          double a = st.r[i];
+          NOC_UNROLL for (int k = 0; k < NX; ++k) a += st.B(k, i) * v[k];
+          Qu[i] = a;
+          Y[i][NX] = a;
+        }
+        kred[1] = ldl_solve<NU, NX + 1>(Quu, Y) ? kred[1] : 0.0;  // Quu > 0 (S:52-53)
+        double Kk[NU * (NX + 1)];
+        NOC_UNROLL for (int i = 0; i < NU; ++i) {
+          NOC_UNROLL for (int j = 0; j < NX; ++j) Kk[i * NX + j] = -Y[i][j];
+          Kk[NU * NX + i] = -Y[i][NX];
+        }
+        NOC_UNROLL for (int i = 0; i < KD; ++i) kds(i, s) = Kk[i];
+        NOC_UNROLL for (int i = 0; i < NU; ++i) {  // dV = k'Qu + 1/2 k'Quu k (S:63)
+          const double ki = Kk[NU * NX + i];
+          double qk = 0.0;
+          NOC_UNROLL for (int j = 0; j < NU; ++j) qk += Quu(i, j) * Kk[NU * NX + j];
+          kred[0] += ki * Qu[i] + 0.5 * ki * qk;
+        }
+        Sym<NX> Sn;  // S <- Q + A'SA + Qux'K ; v <- A'v + Qux'k
+        NOC_UNROLL for (int i = 0; i < NX; ++i)
+          NOC_UNROLL for (int j = i; j < NX; ++j) {
+            double a = st.Q(i, j);
+            NOC_UNROLL for (int k = 0; k < NX; ++k) a += st.A(k, i) * SA(k, j);
+            NOC_UNROLL for (int q = 0; q < NU; ++q) a += Qux(q, i) * Kk[q * NX + j];
+            Sn(i, j) = a;
+          }
+        Vec<NX> vn;
+        NOC_UNROLL for (int i = 0; i < NX; ++i) {
+          double a = 0.0;
+          NOC_UNROLL for (int k = 0; k < NX; ++k) a += st.A(k, i) * v[k];
+          NOC_UNROLL for (int q = 0; q < NU; ++q) a += Qux(q, i) * Kk[NU * NX + q];
+          vn[i] = a;
+        }
+        S = Sn;
+        v = vn;
+        // closed loop of this stage: Phi <- Phi (A + B K), phi <- phi + Phi B k
+        Mat<NX, NX> F;
+        Vec<NX> fv;
+        NOC_UNROLL for (int i = 0; i < NX; ++i) {
+          NOC_UNROLL for (int j = 0; j < NX; ++j) {
+            double a = st.A(i, j);
+            NOC_UNROLL for (int q = 0; q < NU; ++q) a += st.B(i, q) * Kk[q * NX + j];
+            F(i, j) = a;
+          }
+          double a = 0.0;
+          NOC_UNROLL for (int q = 0; q < NU; ++q) a += st.B(i, q) * Kk[NU * NX + q];
+          fv[i] = a;
+        }
+        Mat<NX, NX> Pn;
+        NOC_UNROLL for (int i = 0; i < NX; ++i) {
+          double a = phi[i];
+          NOC_UNROLL for (int k = 0; k < NX; ++k) a += Phi(i, k) * fv[k];
+          phi[i] = a;
+          NOC_UNROLL for (int j = 0; j < NX; ++j) {
+            double c = 0.0;
+            NOC_UNROLL for (int k = 0; k < NX; ++k) c += Phi(i, k) * F(k, j);
+            Pn(i, j) = c;
+          }
+        }
+        Phi = Pn;
+      }
+      {
+        const bool is_max[4] = {false, false, false, false};
+        double kr[4] = {kred[0], 0.0, 0.0, 0.0};
+        NOC_WSUB(3);
+        wg_reduce(kr, 1, is_max);
+        kred[0] = kr[0];
+        kred[1] = __syncthreads_and(kred[1] != 0.0) ? 1.0 : 0.0;
+      }
+      NOC_WSUB(4);
+      const double pred = kred[0];
+      const bool bwd_ok = kred[1] != 0.0;
+      // phase 4: forward affine scan from dx_0 = 0 (P:121-123); thread 0's map is constant
+      if (t == 0) set_zero(Phi);
+#pragma unroll 1
+      for (int d = 1; d < 64; d <<= 1) {
+        Mat<NX, NX> oP;
+        Vec<NX> op;
+        shfl_up_arr<NX * NX>(Phi.v, oP.v, d, 64);
+        shfl_up_arr<NX>(phi.v, op.v, d, 64);
+        if (l >= d) {
+          Mat<NX, NX> Pn;
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            double a = phi[i];
+            NOC_UNROLL for (int k = 0; k < NX; ++k) a += Phi(i, k) * op[k];
+            phi[i] = a;
+            NOC_UNROLL for (int j = 0; j < NX; ++j) {
+              double c = 0.0;
+              NOC_UNROLL for (int k = 0; k < NX; ++k) c += Phi(i, k) * oP(k, j);
+              Pn(i, j) = c;
+            }
+          }
+          Phi = Pn;
+        }
+      }
+      __syncthreads();  // aggregate slots (read by the backward join above)
+      if (l == 63) {
+        NOC_UNROLL for (int i = 0; i < NX * NX; ++i) sagg[wv * 64 + i] = Phi.v[i];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) sagg[wv * 64 + NX * NX + i] = phi[i];
+      }
+      __syncthreads();
+      double xw[NX];  // state at the start of this wave's span
+      NOC_UNROLL for (int i = 0; i < NX; ++i) xw[i] = (wv == 0) ? 0.0 : sagg[NX * NX + i];
+      for (int q = 1; q < wv; ++q) {
+        double xn[NX];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) {
+          double a = sagg[q * 64 + NX * NX + i];
+          NOC_UNROLL for (int k = 0; k < NX; ++k) a += sagg[q * 64 + i * NX + k] * xw[k];
+          xn[i] = a;
+        }
+        NOC_UNROLL for (int i = 0; i < NX; ++i) xw[i] = xn[i];
+      }
+      Vec<NX> x;  // this chunk's start state: lane l-1's inclusive prefix applied to xw
+      {
+        Mat<NX, NX> oP;
+        Vec<NX> op;
+        shfl_up_arr<NX * NX>(Phi.v, oP.v, 1, 64);
+        shfl_up_arr<NX>(phi.v, op.v, 1, 64);
+        NOC_UNROLL for (int i = 0; i < NX; ++i) {
+          double a = op[i];
+          NOC_UNROLL for (int k = 0; k < NX; ++k) a += oP(i, k) * xw[k];
+          x[i] = (l == 0) ? xw[i] : a;
+        }
+      }
+      NOC_WSUB(5);
+      // propagate the chunk: u = K x + d, x+ = A x + B u (the gains are read, then the same LDS
+      // words are overwritten by dx, du -- each stage's K, d only by its own lane)
+      for (int s = start; s < start + len; ++s) {
+        double Kk[KD], A[NX * NX], Bm[NX * NU];
+        NOC_UNROLL for (int i = 0; i < KD; ++i) Kk[i] = kds(i, s);
+        fget<NX * NX>(sA, N, s, A);
+        fget<NX * NU>(sB, N, s, Bm);
+        double u[NU];
+        NOC_UNROLL for (int i = 0; i < NU; ++i) {
+          double a = Kk[NU * NX + i];
+          NOC_UNROLL for (int k = 0; k < NX; ++k) a += Kk[i * NX + k] * x[k];
+          u[i] = a;
+        }
+        double xn[NX];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) {
+          double a = 0.0;
+          NOC_UNROLL for (int k = 0; k < NX; ++k) a += A[i * NX + k] * x[k];
+          NOC_UNROLL for (int j = 0; j < NU; ++j) a += Bm[i * NU + j] * u[j];
+          xn[i] = a;
+        }
+        // the K/d region is [KD][N+1] and dx / du reuse rows 0..NX-1 / NX..NX+NU-1 of it: the
+        // gains of stage s are consumed above before these stores
+        NOC_UNROLL for (int i = 0; i < NX; ++i) dxs(i, s) = x[i];
+        NOC_UNROLL for (int j = 0; j < NU; ++j) dus(j, s) = u[j];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = xn[i];
+      }
+      if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) dxs(i, N) = x[i];
+      __syncthreads();
+      NOC_WSUB(6);
+      NOC_WPHASE(3);
+
+      // ---------------- trial point (P:156-175 / S:121-161) ----------------
+      double tr[4] = {0.0, 0.0, 0.0, 0.0};
+      int ok = 1;
+      for (int s = start; s < start + len; ++s) {
+        double xt[NX], ut[NU];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) xt[i] = sx[(size_t)s * NX + i] + dxs(i, s);
+        NOC_UNROLL for (int j = 0; j < NU; ++j) ut[j] = su[(size_t)j * N + s] + dus(j, s);
+        ok &= f.feasible(ut) ? 1 : 0;
+        tr[0] += f.stage_cost(xt, ut, bp);
+      }
+      if (last) {
+        double xt[NX];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) xt[i] = sx[(size_t)N * NX + i] + dxs(i, N);
+        tr[0] += f.final_cost(xt);
+      }
+      {
+        const bool is_max[4] = {false, false, false, false};
+        wg_reduce(tr, 1, is_max);
+      }
+      const bool traj_ok = __syncthreads_and(ok != 0);
+      const double new_cost = traj_ok ? tr[0] : INFINITY;       // P:159-163, S:126-129
+      const double gain = (new_cost - cost) / pred;             // P:164-165
+      const bool success = (gain > 0.0) && bwd_ok;              // P:166 / S:137
+      const double shrink = fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0));
+      rp = success ? rp * shrink : rp * rinc;                   // P:167-171 / S:139-143
+      rinc = success ? 2.0 : 2.0 * rinc;                        // P:172 / S:144
+      bool take, end_iter, stop;
+      inner += 1;
+      if (mode == NOC_MODE_PAR) {
+        rp = fmin(fmax(rp, 1e-16), 1e16);                       // P:173
+        end_iter = success || inner > 500;                      // P:177-182
+        take = end_iter;                                        // last trial kept (P:175, P:184)
+        stop = end_iter && (hu < 1e-4 || it + 1 > 1000);        // P:199-202
+      } else {
+        take = success;                                         // S:145-146
+        end_iter = true;
+        stop = (hu < 1e-4) && bwd_ok;                           // S:157-161
+      }
+      if (take) {  // x <- x + dx, u <- u + du
+        for (int s = start; s < start + len; ++s) {
+          NOC_UNROLL for (int i = 0; i < NX; ++i) sx[(size_t)s * NX + i] += dxs(i, s);
+          NOC_UNROLL for (int j = 0; j < NU; ++j) su[(size_t)j * N + s] += dus(j, s);
+        }
+        if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) sx[(size_t)N * NX + i] += dxs(i, N);
+      }
+      __syncthreads();
+      NOC_WPHASE(4);
+#ifdef NOC_PERSIST_PROFILE
+      if (b == 0 && t == 0) g_wide_cycles[5] += 1;
+#endif
+      solves += 1;
+      it += end_iter ? 1 : 0;
+      if (stop) {                                               // barrier stage finished
+        total_it += it;                                         // P:239 / S:187
+        bp = bp / 5.0;                                          // P:238 / S:186
+        it = 0;
+        rp = 1.0;                                               // P:134 / S:110
+        rinc = 2.0;                                             // P:135 / S:111
+        stage_done = true;
+      } else if (mode == NOC_MODE_PAR) {
+        relinearize = end_iter;
+      } else {
+        relinearize = success;  // a rejected seq step only changes the regularisation
+      }
+      if (solves >= max_solves) {
+        capped = true;
+        break;
+      }
+    }
+    if (capped || !(bp > 1e-4)) break;                          // P:243-245
+    if (w.flags & NOC_WS_ONE_STAGE) break;                      // newton_oc: one stage
+  }
+  // results out: states, controls, the solver state
+  for (int i = t; i < (N + 1) * NX; i += T) Xg[i] = sx[i];
+  for (int i = t; i < N * NU; i += T) Ug[i] = su[(i % NU) * N + i / NU];
+  if (t == 0) {
+    w.bp[b] = bp;
+    w.rp[b] = rp;
+    w.rinc[b] = rinc;
+    w.cost[b] = cost;
+    w.hu[b] = hu;
+    w.gnorm[b] = gnorm;
+    w.it[b] = it;
+    w.inner[b] = inner;
+    w.total_it[b] = total_it;
+    w.kkt_solves[b] = solves;
+    w.kkt_active[b] = 0;
+    w.phase[b] = capped ? NOC_PHASE_SOLVE : NOC_PHASE_DONE;
+  }
+}
+
+int debug_wide_cycles(long long* out, int n, int reset) {
+  long long host[16];
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wide_cycles), sizeof(host)) != hipSuccess) return -1;
+  for (int i = 0; i < n && i < 16; ++i) out[i] = host[i];
+  if (reset) {
+    const long long zero[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_wide_cycles), zero, sizeof(zero)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+
+// LDS bytes of one wide workgroup, 0 if the trajectory does not fit (one workgroup per CU)
+size_t wide_lds_bytes(int nx, int nu, int N) {
+  int total = 0;
+#define NOC_FAMILY(K, X, U) \
+  if (nx == X && nu == U) total = WideLds<X, U>(N, kWideWaves).total;
+#include NOC_FAMILIES_DEF
+#undef NOC_FAMILY
+  if (total == 0) return 0;
+  const size_t bytes = (size_t)total * sizeof(double);
+  return bytes <= 160 * 1024 - 1024 ? bytes : 0;
+}
+
+template <int K, int X, int U>
+static hipError_t wide_family(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                              double bp0, int max_solves, hipStream_t s) {
+  if constexpr (X <= 4) {
+    const size_t lds = wide_lds_bytes(X, U, w.N);
+    if (lds == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((ipm_wide_kernel<K, X, U, kWideWaves>), dim3(w.Bt), dim3(64 * kWideWaves), lds,
+                       s, p, w, mode, terminal, bp0, max_solves);
+    return hipGetLastError();
+  } else {
+    return hipErrorInvalidValue;
+  }
+}
+
+bool ipm_wide_supported(const noc_family& p, int N) {
+  return family_supported(p) && p.nx <= 4 && wide_lds_bytes(p.nx, p.nu, N) > 0;
+}
+
+hipError_t ipm_solve_wide(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                          double bp0, int max_solves, hipStream_t s) {
+#define NOC_FAMILY(K, X, U)                                                              \
+  if (p.kind == K && p.nx == X && p.nu == U)                                             \
+    return wide_family<K, X, U>(p, w, mode, terminal, bp0, max_solves, s);
+#include NOC_FAMILIES_DEF
+#undef NOC_FAMILY
+  return hipErrorInvalidValue;
+}
+
+}  // namespace noc

@@ -282,12 +282,23 @@ NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st, double reg) {
 // stream, and no shuffle ever reads an EXEC-masked lane.
 // VALUE_ONLY: every right operand is value-only (the last level: partner l + L/2 covers the end),
 // so the result is value-only too and only J, nu are formed (T A1 is the only solve needed).
-template <int NX, bool VALUE_ONLY>
+// PAD_IDENTITY: partner-less lanes combine with the identity element (A = I, b = C = nu = J = 0)
+// instead of themselves, which leaves them unchanged exactly -- for segments whose last lane does
+// NOT end at the terminal cost (the waves of a multi-wave trajectory, ipm_wide.hip).
+template <int NX, bool VALUE_ONLY, bool PAD_IDENTITY = false>
 NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
   Sym<NX> J2;
   Vec<NX> nu2;
-  shfl_down_arr<Sym<NX>::SZ>(e1.J.v, J2.v, d, L);
-  shfl_down_arr<NX>(e1.nu.v, nu2.v, d, L);
+  const bool pad = PAD_IDENTITY && (int)(__lane_id() % L) + d >= L;
+  auto fetch_value = [&]() {
+    shfl_down_arr<Sym<NX>::SZ>(e1.J.v, J2.v, d, L);
+    shfl_down_arr<NX>(e1.nu.v, nu2.v, d, L);
+    if (pad) {
+      set_zero(J2);
+      set_zero(nu2);
+    }
+  };
+  fetch_value();
   constexpr int NR = VALUE_ONLY ? NX : 2 * NX + 1;
   double X[NX][NX];
   double Y[NX][NR];
@@ -326,8 +337,7 @@ NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
   // the solve with partial pivoting.  J2 / nu2 are re-fetched there instead of kept live.
   const bool ok = lu_np_solve<NX, NR>(X, Y);
   if (__any(!ok)) {
-    shfl_down_arr<Sym<NX>::SZ>(e1.J.v, J2.v, d, L);
-    shfl_down_arr<NX>(e1.nu.v, nu2.v, d, L);
+    fetch_value();
     build();
     lu_pp_solve<NX, NR>(X, Y);
   }
@@ -354,6 +364,11 @@ NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
     shfl_down_arr<NX * NX>(e1.A.v, A2.v, d, L);
     shfl_down_arr<NX>(e1.b.v, b2.v, d, L);
     shfl_down_arr<Sym<NX>::SZ>(e1.C.v, C2.v, d, L);
+    if (pad) {
+      set_identity(A2);
+      set_zero(b2);
+      set_zero(C2);
+    }
     // A = A2 TA ; b = A2 Tb + b2 ; C = A2 TC A2' + C2
     Mat<NX, NX> T2;  // A2 * TC
     NOC_UNROLL for (int i = 0; i < NX; ++i) {

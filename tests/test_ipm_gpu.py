@@ -177,9 +177,11 @@ def test_linear_demo_known_answer():
 
 @pytest.mark.parametrize("name,N,Bt", [("pendulum", 60, 16), ("cartpole", 200, 64)])
 @pytest.mark.parametrize("mode", ["par", "seq"])
-def test_persistent_solve_equals_multilaunch_loop(name, N, Bt, mode):
+def test_persistent_solve_equals_multilaunch_loop(name, N, Bt, mode, monkeypatch):
     """noc_ipm_solve (whole solve in one launch, one wave per trajectory) against the multi-launch
-    device loop at the same lanes (64): same arithmetic, so identical counters and iterates."""
+    device loop at the same lanes (64): same arithmetic, so identical counters and iterates.
+    (The one-wave kernel is forced: small batches default to the wide kernel.)"""
+    monkeypatch.setenv("NOC_PERSIST_WIDE", "0")
     from noc import problems, _lib
     from noc.ipm import BatchedIPM
     ocp = problems.make_problem(name, N)
@@ -198,8 +200,11 @@ def test_persistent_solve_equals_multilaunch_loop(name, N, Bt, mode):
     assert np.max(np.abs(Up - Um)) <= 1e-12 * max(1.0, float(np.max(np.abs(Um))))
 
 
-def test_persistent_solve_respects_solve_cap():
-    """A trajectory that reaches max_solves stops (phase != DONE) -- every wave exits."""
+@pytest.mark.parametrize("wide", ["0", "1"])
+def test_persistent_solve_respects_solve_cap(wide, monkeypatch):
+    """A trajectory that reaches max_solves stops (phase != DONE) -- every wave exits (the one-wave
+    and the wide kernel)."""
+    monkeypatch.setenv("NOC_PERSIST_WIDE", wide)
     from noc import problems, _lib
     from noc.ipm import BatchedIPM
     N, Bt = 50, 8
@@ -211,6 +216,41 @@ def test_persistent_solve_respects_solve_cap():
     torch.cuda.synchronize()
     assert np.all(eng.t["kkt_solves"].cpu().numpy() == 5)
     assert np.all(eng.t["phase"].cpu().numpy() != _lib.PHASE_DONE)
+
+
+@pytest.mark.parametrize("name,N,Bt,mode", [
+    ("pendulum", 60, 16, "par"), ("pendulum", 60, 16, "seq"),
+    ("pendulum", 20, 4, "par"),      # N < 64: most lanes of every wave own no stage
+    ("cartpole", 200, 8, "par"), ("cartpole", 200, 8, "seq"),
+    ("cartpole", 300, 3, "par"),     # N > 256: two stages on some lanes
+    ("linear2", 100, 5, "par"),
+])
+def test_wide_solve_matches_one_wave_kernel(name, N, Bt, mode, monkeypatch):
+    """The wide whole-solve kernel (ipm_wide.hip: four waves per trajectory, blocks in LDS) against
+    the one-wave kernel on the same inputs: identical outer iterations / KKT solves per trajectory,
+    controls within 1e-8 relative (the scans associate differently, so not bit-identical)."""
+    from noc import problems, _lib
+    from noc.ipm import BatchedIPM
+    if name == "linear2":  # box-constrained double integrator (the LINEAR family's log barrier)
+        ocp = problems.double_integrators(1, 0.01, constrained=True)
+        x0 = np.random.default_rng(33).normal(size=(Bt, 2))
+        u0 = np.zeros((Bt, N, 1))
+    else:
+        ocp = problems.make_problem(name, N)
+        x0, u0 = problems.initial_conditions(name, N, Bt, seed=33)
+    m = _lib.MODE_PAR if mode == "par" else _lib.MODE_SEQ
+    res = []
+    for wide in ("1", "0"):
+        monkeypatch.setenv("NOC_PERSIST_WIDE", wide)
+        eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
+        eng.load(u0, x0)
+        eng.solve(mode=m)
+        torch.cuda.synchronize()
+        res.append([t.cpu().numpy() for t in eng.result()] + [eng.t["phase"].cpu().numpy()])
+    (Uw, itw, sw, phw), (Un, itn, sn, phn) = res
+    assert np.array_equal(itw, itn) and np.array_equal(sw, sn), (itw, itn, sw, sn)
+    assert np.all(phw == _lib.PHASE_DONE)
+    assert np.max(np.abs(Uw - Un)) <= 1e-8 * max(1.0, float(np.max(np.abs(Un))))
 
 
 def test_linear8_ipm_uses_group_solve_and_is_exact():
