@@ -15,6 +15,32 @@ import contextlib
 
 import numpy as np
 import sympy as sp
+from sympy.printing.c import C99CodePrinter
+from sympy.printing.precedence import PRECEDENCE
+
+
+class _DevicePrinter(C99CodePrinter):
+    """sympy's C printer, except that small integer powers become products (x^2 -> (x*x),
+    x^-2 -> 1.0/(x*x)) and x^(+-1/2) sqrt: pow() on the device is the general double-double
+    exp/log routine -- ~200 instructions per call, which dominated the Euler step of the rollout's
+    sequential chain -- where a product is one correctly rounded multiply."""
+
+    def _print_Pow(self, expr, rational=False):
+        b, e = expr.base, expr.exp
+        if e.is_Integer and 1 <= abs(int(e)) <= 8:
+            n = abs(int(e))
+            base = self.parenthesize(b, PRECEDENCE["Mul"] + 1)
+            prod = "*".join([base] * n) if n > 1 else base
+            return f"({prod})" if int(e) > 0 else f"(1.0/({prod}))"
+        if e == sp.Rational(1, 2):
+            return f"sqrt({self._print(b)})"
+        if e == sp.Rational(-1, 2):
+            return f"(1.0/sqrt({self._print(b)}))"
+        return super()._print_Pow(expr, rational=rational)
+
+
+def _ccode(e) -> str:
+    return _DevicePrinter().doprint(e)
 
 
 def _trig_subst(exprs, X):
@@ -53,8 +79,8 @@ def emit(name, X, U, f):
         for i in range(len(U)):
             lines.append(f"  [[maybe_unused]] const double u{i} = u[{i}];")
         lines.extend(pre)
-        lines.extend(f"  const double {sp.ccode(s)} = {sp.ccode(e)};" for s, e in reps)
-        lines.extend(f"  {t} = {sp.ccode(e)};" for t, e in zip(targets, red))
+        lines.extend(f"  const double {_ccode(s)} = {_ccode(e)};" for s, e in reps)
+        lines.extend(f"  {t} = {_ccode(e)};" for t, e in zip(targets, red))
         lines.append("}")
 
     block(f"NOC_DEV void {name}_ode(const double* x, const double* u, double* f)",
