@@ -151,6 +151,11 @@ typedef struct noc_family {
 /* Workspace of device pointers (all fp64 unless noted; Bt trajectories, horizon N). */
 #define NOC_WS_ONE_STAGE 1 /* flags bit: stop after ONE barrier stage (newton_oc, P:127-225 /
                               S:108-177) instead of running the schedule while bp > 1e-4 */
+#define NOC_WS_RESUME 2    /* flags bit (noc_ipm_solve): continue every trajectory from the state
+                              held in the workspace (bp, rp, r_inc, cost, hu, gnorm, it, inner,
+                              total_it, kkt_solves, x, u) at its phase -- ROLLOUT: a new barrier
+                              stage, LINEARIZE: a new Newton iteration, SOLVE: a retry on the
+                              current blocks, DONE: nothing -- instead of starting at bp0 */
 typedef struct noc_ipm_ws {
   int Bt, N;
   int lanes;                           /* tiled layout of A,B,Q,R,M,r,K,d (8/16/32/64)  */
@@ -206,6 +211,10 @@ int noc_ipm_solve_supported(const noc_family* fam, int N, int lanes);
  * reduction, forward scan, propagate); all zero unless the library was built with
  * -DNOC_PERSIST_PROFILE.  reset != 0 zeroes them after reading.  Synchronous. */
 int noc_debug_phase_cycles(long long* out, int n, int reset);
+/* Timing-only: start / end stamps (s_memrealtime, 100 MHz) of trajectories 0..n-1 of the last
+ * one-wave persistent solve, out[2b], out[2b+1] (n <= 16384); zeros unless the library was built
+ * with -DNOC_PERSIST_PROFILE.  Synchronous. */
+int noc_debug_traj_times(long long* out, int n);
 int noc_ipm_solve(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, double bp0,
                   int max_solves, void* stream);
 

@@ -22,8 +22,12 @@ namespace noc {
 constexpr double kTwoPi = 6.283185307179586;  // 2.0 * jnp.pi
 
 // noc/utils.py:8-10 with jnp.remainder semantics (C fmod, + divisor if the sign differs)
+// fmod(a, 2 pi) == a exactly for |a| < 2 pi, so the general fmod routine (~70 instructions, a
+// loop) only runs for lanes outside that range -- a branch, not a select, so a wave whose angles
+// all lie in (-2 pi, 2 pi) skips it.
 NOC_DEV double wrap_angle(double a) {
-  double r = fmod(a, kTwoPi);
+  double r = a;
+  if (__builtin_expect(!(fabs(a) < kTwoPi), 0)) r = fmod(a, kTwoPi);
   return (r != 0.0 && r < 0.0) ? r + kTwoPi : r;
 }
 
@@ -177,6 +181,15 @@ NOC_DEV double readlane_d(double v, int lane) {  // wave-uniform broadcast of on
 // max that propagates NaN like jnp.max (fmax drops it): a NaN |Hu| must fail the < 1e-4 stop
 // test exactly as in the reference (P:158, P:199; D:120)
 NOC_DEV double nan_max(double a, double b) { return (a != a || b != b) ? NAN : fmax(a, b); }
+
+// The phase a persistent solve resumes at (NOC_WS_RESUME) from a workspace phase, including the
+// two-stream driver's intermediate ones: ROLLED (states current) continues with a new Newton
+// iteration, ROLLOUT_PENDING with the rollout.
+NOC_DEV int resume_phase(int ph) {
+  if (ph == NOC_PHASE_ROLLED) return NOC_PHASE_LINEARIZE;
+  if (ph == NOC_PHASE_ROLLOUT_PENDING) return NOC_PHASE_ROLLOUT;
+  return ph;
+}
 
 NOC_DEV double wave_sum(double v) {
   NOC_UNROLL for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

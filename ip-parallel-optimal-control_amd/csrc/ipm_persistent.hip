@@ -29,6 +29,11 @@ namespace noc {
 // -DNOC_PERSIST_PROFILE, read back by noc_debug_phase_cycles): rollout, linearise, costate +
 // blocks, KKT scan, trial, number of Newton iterations.
 __device__ long long g_phase_cycles[8];
+// Start / end wall-clock stamps (s_memrealtime, 100 MHz) of every trajectory's persistent solve,
+// same builds only (read back by noc_debug_traj_times): the batch's schedule, e.g. when the
+// straggler that sets the wall time started and how its neighbours thinned out.
+constexpr int kTrajStamps = 16384;
+__device__ long long g_traj_times[kTrajStamps][2];
 
 namespace {
 constexpr int PL = 64;  // lanes per trajectory in the persistent solver
@@ -57,7 +62,9 @@ NOC_DEV IpmState* state_slot(int N) {
 // WPS: waves per SIMD the register budget is sized for.  2 = 256 registers per lane; 1 = 512, the
 // upper half AGPRs, which the compiler uses as spill space instead of scratch (cart-pole: 460 B
 // of scratch per lane at WPS = 2, none at WPS = 1), and which pays for the stage pairs below.
-template <int KIND, int NX, int NU, int WPS>
+// RESUME: continue from the workspace state (NOC_WS_RESUME; its own instance, so the plain solve's
+// register allocation does not carry the resume bookkeeping).
+template <int KIND, int NX, int NU, int WPS, bool RESUME>
 __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
                                                          int terminal, double bp0,
                                                          int max_solves) {
@@ -94,15 +101,24 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
   double bp = bp0, rp = 1.0, rinc = 2.0, cost = 0.0, hu = 1.0, gnorm = 0.0;
   int it = 0, inner = 0, total_it = 0, solves = 0;
   bool capped = false;
+  int phase = NOC_PHASE_DONE;     // the resume point a capped launch leaves in the workspace
+  int entry = NOC_PHASE_ROLLOUT;  // RESUME: where this launch starts
+  if constexpr (RESUME) {
+    bp = w.bp[b]; rp = w.rp[b]; rinc = w.rinc[b]; cost = w.cost[b]; hu = w.hu[b];
+    gnorm = w.gnorm[b]; it = w.it[b]; inner = w.inner[b]; total_it = w.total_it[b];
+    solves = w.kkt_solves[b]; entry = resume_phase(w.phase[b]);
+    if (entry == NOC_PHASE_DONE) return;  // uniform over the wave
+  }
 
 #ifdef NOC_PERSIST_PROFILE
   long long t_prev = clock64();
+  if (l == 0 && b < kTrajStamps) g_traj_times[b][0] = (long long)__builtin_amdgcn_s_memrealtime();
 #endif
   for (;;) {  // ---------------- barrier stages (P:228-254) ----------------
     // rollout x_{k+1} = f(x_k, u_k) (noc/utils.py:57-63, P:133): every lane runs the recurrence
     // redundantly with u_k broadcast by readlane; lane t stores the states of block step t
     wave_fence();  // u was last written chunk-wise by the trials
-    {
+    if (!RESUME || entry == NOC_PHASE_ROLLOUT) {
       double x[NX];
       NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = w.x0[(size_t)b * NX + i];
       if (l < NX) X[l] = x[l];
@@ -127,7 +143,8 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
     }
     wave_fence();  // states of every stage visible to their chunk owners
     NOC_PHASE(0);
-    bool relinearize = true;
+    bool relinearize = !RESUME || entry != NOC_PHASE_SOLVE;  // SOLVE: the ws blocks are current
+    if constexpr (RESUME) entry = NOC_PHASE_ROLLOUT;
     bool stage_done = false;
     while (!stage_done) {  // ---------------- Newton iterations (P:127-225) ----------------
       if (relinearize) {
@@ -436,8 +453,10 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       } else {
         relinearize = success;  // a rejected seq step only changes the regularisation
       }
-      if (solves >= max_solves) {
+      if (solves >= max_solves) {  // capped: record where a later launch continues
         capped = true;
+        phase = stage_done ? NOC_PHASE_ROLLOUT : (relinearize ? NOC_PHASE_LINEARIZE : NOC_PHASE_SOLVE);
+        if (stage_done && (!(bp > 1e-4) || (w.flags & NOC_WS_ONE_STAGE))) phase = NOC_PHASE_DONE;
         break;
       }
     }
@@ -456,7 +475,10 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
     w.total_it[b] = total_it;
     w.kkt_solves[b] = solves;
     w.kkt_active[b] = 0;
-    w.phase[b] = capped ? NOC_PHASE_SOLVE : NOC_PHASE_DONE;
+    w.phase[b] = phase;
+#ifdef NOC_PERSIST_PROFILE
+    if (b < kTrajStamps) g_traj_times[b][1] = (long long)__builtin_amdgcn_s_memrealtime();
+#endif
   }
 }
 
@@ -494,13 +516,21 @@ static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, in
     static const char* env = getenv("NOC_PERSIST_WAVES");
     const bool one = env ? atoi(env) == 1 : (simds > 0 && w.Bt <= simds);
     if (one) {
-      hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 1>), dim3(w.Bt), dim3(64), lds, s, p, w,
-                         mode, terminal, bp0, max_solves);
+      if (w.flags & NOC_WS_RESUME)
+        hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 1, true>), dim3(w.Bt), dim3(64), lds, s,
+                           p, w, mode, terminal, bp0, max_solves);
+      else
+        hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 1, false>), dim3(w.Bt), dim3(64), lds, s,
+                           p, w, mode, terminal, bp0, max_solves);
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 2>), dim3(w.Bt), dim3(64), lds, s, p, w, mode,
-                     terminal, bp0, max_solves);
+  if (w.flags & NOC_WS_RESUME)
+    hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 2, true>), dim3(w.Bt), dim3(64), lds, s, p,
+                       w, mode, terminal, bp0, max_solves);
+  else
+    hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 2, false>), dim3(w.Bt), dim3(64), lds, s, p,
+                       w, mode, terminal, bp0, max_solves);
   return hipGetLastError();
 }
 
@@ -515,6 +545,13 @@ int debug_phase_cycles(long long* out, int n, int reset) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), zero, sizeof(zero)) != hipSuccess) return -1;
   }
   return 0;
+}
+
+int debug_traj_times(long long* out, int n) {
+  if (n > kTrajStamps) n = kTrajStamps;
+  if (n <= 0) return 0;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_traj_times), (size_t)n * 2 * sizeof(long long)) ==
+                 hipSuccess ? 0 : -1;
 }
 
 // persistent instances exist for the families with nx <= 4 (an nx = 8 scan element does not fit a
@@ -541,6 +578,8 @@ static hipError_t solve_family(const noc_family& p, const noc_ipm_ws& w, int mod
 
 // The wide kernel (ipm_wide.hip: 4 waves and the LDS of one CU per trajectory) when the batch
 // leaves CUs idle anyway (B <= #CUs: the reference's B = 1 runs); NOC_PERSIST_WIDE=0|1 overrides.
+// (Re-packing the last <= #CUs trajectories of a large batch onto it was measured and dropped:
+// those are Newton retries, KKT-bound, and the wide KKT solve is no faster -- DESIGN.md §3.7.)
 static bool use_wide(const noc_family& p, const noc_ipm_ws& w) {
   const char* env = getenv("NOC_PERSIST_WIDE");
   if (env && atoi(env) == 0) return false;
@@ -552,7 +591,8 @@ static bool use_wide(const noc_family& p, const noc_ipm_ws& w) {
 
 hipError_t ipm_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal, double bp0,
                      int max_solves, hipStream_t s) {
-  if (use_wide(p, w)) return ipm_solve_wide(p, w, mode, terminal, bp0, max_solves, s);
+  if (use_wide(p, w))
+    return ipm_solve_wide(p, w, mode, terminal, bp0, max_solves, nullptr, nullptr, w.Bt, s);
 #define NOC_FAMILY(K, X, U)                                                              \
   if (p.kind == K && p.nx == X && p.nu == U)                                             \
     return solve_family<K, X, U>(p, w, mode, terminal, bp0, max_solves, s);

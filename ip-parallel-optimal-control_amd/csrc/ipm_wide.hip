@@ -150,19 +150,22 @@ NOC_DEV void elem_get(const double* p, Elem<NX>& e) {
 
 }  // namespace
 
-// W waves per trajectory (blockDim = 64 W), one workgroup per trajectory.
+// W waves per trajectory (blockDim = 64 W), one workgroup per trajectory at a time: workgroup g
+// solves trajectories idx[g], idx[g + grid], ... of the *count listed (idx == NULL: 0..Bt-1).
 template <int KIND, int NX, int NU, int W>
 __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc_ipm_ws w, int mode,
                                                              int terminal, double bp0,
-                                                             int max_solves) {
+                                                             int max_solves, const int* idx,
+                                                             const int* count) {
   constexpr int T = 64 * W;
   constexpr int KD = NU * (NX + 1);
   constexpr int ESZ = NX * NX + 2 * NX + 2 * Sym<NX>::SZ;  // scan element in doubles
   static_assert(ESZ <= 64 && NX * NX + NX <= 64, "aggregate slot");
   extern __shared__ __attribute__((aligned(16))) double noc_smem[];
-  const int b = blockIdx.x;
   const int t = threadIdx.x, wv = t >> 6, l = t & 63;
-  if (b >= w.Bt) return;  // uniform over the workgroup
+  const int n_traj = count ? *count : w.Bt;
+  for (int jb = blockIdx.x; jb < n_traj; jb += gridDim.x) {  // uniform over the workgroup
+  const int b = idx ? idx[jb] : jb;
   Fam<KIND, NX, NU> f(prm);
   const int N = w.N;
   const WideLds<NX, NU> L(N, W);
@@ -220,14 +223,26 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
 
   double bp = bp0, rp = 1.0, rinc = 2.0, cost = 0.0, hu = 1.0, gnorm = 0.0;
   int it = 0, inner = 0, total_it = 0, solves = 0;
-  bool capped = false;
+  int phase = NOC_PHASE_ROLLOUT;  // where this launch starts (NOC_WS_RESUME) / stopped
+  if (w.flags & NOC_WS_RESUME) {
+    bp = w.bp[b]; rp = w.rp[b]; rinc = w.rinc[b]; cost = w.cost[b]; hu = w.hu[b];
+    gnorm = w.gnorm[b]; it = w.it[b]; inner = w.inner[b]; total_it = w.total_it[b];
+    solves = w.kkt_solves[b]; phase = resume_phase(w.phase[b]);
+  }
+  if (phase == NOC_PHASE_DONE) continue;  // uniform; no LDS written yet
+  // resuming inside a barrier stage: the states are the workspace's (the blocks are recomputed
+  // from them -- the same values -- but a SOLVE resume keeps its retry counter)
+  bool keep_inner = phase == NOC_PHASE_SOLVE;
+  if (phase != NOC_PHASE_ROLLOUT)
+    for (int i = t; i < (N + 1) * NX; i += T) sx[i] = Xg[i];
+  __syncthreads();
 #ifdef NOC_PERSIST_PROFILE
   long long t_prev = clock64();
 #endif
 
   for (;;) {  // ---------------- barrier stages (P:228-254) ----------------
     // rollout (U:57-63, P:133): wave 0 runs the recurrence, lane (k mod 64) keeps stage k
-    if (wv == 0) {
+    if (phase == NOC_PHASE_ROLLOUT && wv == 0) {
       double x[NX];
       NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = w.x0[(size_t)b * NX + i];
       if (l < NX) sx[l] = x[l];
@@ -397,7 +412,8 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
         cost = red[0] + f.final_cost(xN);  // total_cost(x, u, bp) (P:142)
         hu = red[1];                       // max |Hu| (P:158)
         gnorm = sqrt(red[2]);              // ||cu||_F (P:116)
-        inner = 0;
+        if (!keep_inner) inner = 0;
+        keep_inner = false;
         relinearize = false;
       }
       const double reg = (mode == NOC_MODE_PAR) ? rp * gnorm : rp;  // P:116-118 / S:51
@@ -726,13 +742,12 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
       } else {
         relinearize = success;  // a rejected seq step only changes the regularisation
       }
-      if (solves >= max_solves) {
-        capped = true;
-        break;
-      }
+      // where a later launch would continue (the resume point)
+      phase = stage_done ? NOC_PHASE_ROLLOUT : (relinearize ? NOC_PHASE_LINEARIZE : NOC_PHASE_SOLVE);
+      if (stage_done && (!(bp > 1e-4) || (w.flags & NOC_WS_ONE_STAGE))) phase = NOC_PHASE_DONE;
+      if (phase == NOC_PHASE_DONE || solves >= max_solves) break;
     }
-    if (capped || !(bp > 1e-4)) break;                          // P:243-245
-    if (w.flags & NOC_WS_ONE_STAGE) break;                      // newton_oc: one stage
+    if (phase != NOC_PHASE_ROLLOUT || solves >= max_solves) break;  // P:243-245 / capped
   }
   // results out: states, controls, the solver state
   for (int i = t; i < (N + 1) * NX; i += T) Xg[i] = sx[i];
@@ -749,7 +764,9 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
     w.total_it[b] = total_it;
     w.kkt_solves[b] = solves;
     w.kkt_active[b] = 0;
-    w.phase[b] = capped ? NOC_PHASE_SOLVE : NOC_PHASE_DONE;
+    w.phase[b] = phase;
+  }
+  __syncthreads();  // the next trajectory's controls overwrite the LDS read above
   }
 }
 
@@ -778,12 +795,13 @@ size_t wide_lds_bytes(int nx, int nu, int N) {
 
 template <int K, int X, int U>
 static hipError_t wide_family(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
-                              double bp0, int max_solves, hipStream_t s) {
+                              double bp0, int max_solves, const int* idx, const int* count,
+                              int grid, hipStream_t s) {
   if constexpr (X <= 4) {
     const size_t lds = wide_lds_bytes(X, U, w.N);
-    if (lds == 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((ipm_wide_kernel<K, X, U, kWideWaves>), dim3(w.Bt), dim3(64 * kWideWaves), lds,
-                       s, p, w, mode, terminal, bp0, max_solves);
+    if (lds == 0 || grid <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((ipm_wide_kernel<K, X, U, kWideWaves>), dim3(grid), dim3(64 * kWideWaves),
+                       lds, s, p, w, mode, terminal, bp0, max_solves, idx, count);
     return hipGetLastError();
   } else {
     return hipErrorInvalidValue;
@@ -795,10 +813,11 @@ bool ipm_wide_supported(const noc_family& p, int N) {
 }
 
 hipError_t ipm_solve_wide(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
-                          double bp0, int max_solves, hipStream_t s) {
+                          double bp0, int max_solves, const int* idx, const int* count, int grid,
+                          hipStream_t s) {
 #define NOC_FAMILY(K, X, U)                                                              \
   if (p.kind == K && p.nx == X && p.nu == U)                                             \
-    return wide_family<K, X, U>(p, w, mode, terminal, bp0, max_solves, s);
+    return wide_family<K, X, U>(p, w, mode, terminal, bp0, max_solves, idx, count, grid, s);
 #include NOC_FAMILIES_DEF
 #undef NOC_FAMILY
   return hipErrorInvalidValue;

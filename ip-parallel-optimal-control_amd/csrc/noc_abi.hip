@@ -348,6 +348,11 @@ int noc_debug_phase_cycles(long long* out, int n, int reset) {
   return noc::debug_phase_cycles(out, n, reset) == 0 ? 0 : fail(-10, "hipMemcpyFromSymbol failed");
 }
 
+int noc_debug_traj_times(long long* out, int n) {
+  if (!out || n < 0) return fail(-2, "out is NULL");
+  return noc::debug_traj_times(out, n) == 0 ? 0 : fail(-10, "hipMemcpyFromSymbol failed");
+}
+
 int noc_ipm_solve_supported(const noc_family* fam, int N, int lanes) {
   return (fam && N >= 1 && noc::ipm_solve_supported(*fam, N, lanes)) ? 1 : 0;
 }

@@ -52,6 +52,7 @@ class NocFamily(ctypes.Structure):
 WS_DOUBLE_FIELDS = ["x", "u", "x0", "A", "B", "Q", "R", "M", "r", "P", "cx", "cu", "lc", "lam",
                     "dx", "du", "pred", "K", "d"]
 WS_ONE_STAGE = 1  # NocIpmWs.flags bit: stop after one barrier stage (newton_oc)
+WS_RESUME = 2  # NocIpmWs.flags bit: noc_ipm_solve continues from the workspace state
 WS_INT_FIELDS = ["feasible", "phase", "kkt_active", "it", "inner", "total_it", "kkt_solves"]
 WS_STATE_FIELDS = ["bp", "rp", "rinc", "cost", "hu", "gnorm", "reg"]
 
@@ -75,6 +76,7 @@ SIGNATURES.update({
     "noc_ipm_promote": (_i, [_wp, _dp]),
     "noc_ipm_solve_supported": (_i, [_fp, _i, _i]),
     "noc_debug_phase_cycles": (_i, [ctypes.POINTER(ctypes.c_longlong), _i, _i]),
+    "noc_debug_traj_times": (_i, [ctypes.POINTER(ctypes.c_longlong), _i]),
     "noc_ipm_solve": (_i, [_fp, _wp, _i, _i, ctypes.c_double, _i, _dp]),
     "noc_derivatives": (_i, [_fp, _i, _i] + [_dp] * 13 + [_dp]),
     "noc_final_cost_derivs": (_i, [_fp, _i, _dp, _dp, _dp, _dp]),

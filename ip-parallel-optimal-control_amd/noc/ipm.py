@@ -140,14 +140,22 @@ class BatchedIPM:
         return self.active_count() == 0
 
     def solve_persistent(self, mode: int = _lib.MODE_PAR, terminal: Optional[int] = None,
-                         bp0: float = 0.1, max_solves: int = 10 ** 7):
+                         bp0: float = 0.1, max_solves: int = 10 ** 7, resume: bool = False):
         """The whole barrier schedule of every trajectory in ONE launch (noc_ipm_solve).
         Returns the KKT solves of the slowest trajectory (the multi-launch loop's step count).
-        terminal=None: the reference's choice for the mode (par: XT = Q[0], P:73; seq: S:66)."""
+        terminal=None: the reference's choice for the mode (par: XT = Q[0], P:73; seq: S:66).
+        resume=True continues every trajectory from the workspace state a previous (capped)
+        solve left (NOC_WS_RESUME); max_solves counts the solves of both."""
         terminal = default_terminal(mode) if terminal is None else terminal
-        _lib.check(self._lib.noc_ipm_solve(ctypes.byref(self.fam_c), ctypes.byref(self.ws), mode,
-                                           terminal, float(bp0), int(max_solves), self._stream()),
-                   "noc_ipm_solve", self._lib)
+        flags = self.ws.flags
+        if resume:
+            self.ws.flags = flags | _lib.WS_RESUME
+        try:
+            _lib.check(self._lib.noc_ipm_solve(ctypes.byref(self.fam_c), ctypes.byref(self.ws),
+                                               mode, terminal, float(bp0), int(max_solves),
+                                               self._stream()), "noc_ipm_solve", self._lib)
+        finally:
+            self.ws.flags = flags
         return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
 
     def solve(self, mode: int = _lib.MODE_PAR, terminal: Optional[int] = None,

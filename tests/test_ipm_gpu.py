@@ -253,6 +253,46 @@ def test_wide_solve_matches_one_wave_kernel(name, N, Bt, mode, monkeypatch):
     assert np.max(np.abs(Uw - Un)) <= 1e-8 * max(1.0, float(np.max(np.abs(Un))))
 
 
+def _resume_case(name, N, Bt, seed=5):
+    from noc import problems
+    ocp = problems.make_problem(name, N)
+    x0, u0 = problems.initial_conditions(name, N, Bt, seed=seed)
+    return ocp, x0, u0
+
+
+@pytest.mark.parametrize("wide", ["0", "1"])
+@pytest.mark.parametrize("name,N,Bt,mode,caps", [
+    ("pendulum", 60, 16, "par", (5, 37, 60)),
+    ("pendulum", 60, 16, "seq", (3, 50)),
+    ("cartpole", 200, 6, "par", (1, 90, 91, 180)),
+])
+def test_capped_then_resumed_solve_equals_uninterrupted(name, N, Bt, mode, caps, wide, monkeypatch):
+    """noc_ipm_solve stopped by max_solves and continued with NOC_WS_RESUME (as often as the caps
+    say) gives exactly the uninterrupted solve: identical counters and controls, bit for bit --
+    for the one-wave kernel (its blocks stay in the workspace) and the wide kernel (it recomputes
+    them from the workspace states with the same arithmetic)."""
+    monkeypatch.setenv("NOC_PERSIST_WIDE", wide)
+    from noc import _lib
+    from noc.ipm import BatchedIPM
+    ocp, x0, u0 = _resume_case(name, N, Bt)
+    m = _lib.MODE_PAR if mode == "par" else _lib.MODE_SEQ
+    ref = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
+    ref.load(u0, x0)
+    ref.solve_persistent(mode=m)
+    eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
+    eng.load(u0, x0)
+    for i, cap in enumerate(caps):
+        eng.solve_persistent(mode=m, max_solves=cap, resume=i > 0)
+        torch.cuda.synchronize()
+        assert int(eng.t["kkt_solves"].max().item()) <= cap
+    eng.solve_persistent(mode=m, resume=True)
+    torch.cuda.synchronize()
+    for k in ("u", "x", "kkt_solves", "total_it", "phase", "bp", "rp"):
+        a, b = eng.t[k].cpu().numpy(), ref.t[k].cpu().numpy()
+        assert np.array_equal(a, b), (k, np.max(np.abs(a.astype(float) - b.astype(float))))
+    assert np.all(eng.t["phase"].cpu().numpy() == _lib.PHASE_DONE)
+
+
 def test_linear8_ipm_uses_group_solve_and_is_exact():
     """Four stacked double integrators (nx=8, nu=4; the c4 family): the IPM workspace defaults to
     the grouped layout + horizon-sequential group solve (lanes 1); the unconstrained LQ problem is
