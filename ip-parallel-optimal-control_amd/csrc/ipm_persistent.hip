@@ -577,7 +577,11 @@ static hipError_t solve_family(const noc_family& p, const noc_ipm_ws& w, int mod
 }
 
 // The wide kernel (ipm_wide.hip: 4 waves and the LDS of one CU per trajectory) when the batch
-// leaves CUs idle anyway (B <= #CUs: the reference's B = 1 runs); NOC_PERSIST_WIDE=0|1 overrides.
+// leaves CUs idle anyway (B <= #CUs: the reference's B = 1 runs) and the horizon gives the
+// one-wave kernel more than two stages per lane: at N <= 128 the one-wave solve is faster (its
+// KKT scan needs no cross-wave join), beyond it the wide one (B = 1, per KKT solve: pendulum
+// N=200 16.5 vs 20.4 us, N=800 32 vs 57 us; cart-pole N=128 31.6 vs 25.7 us, N=200 33.0 vs
+// 35.2 us -- profiles/r02/wide/crossover.jsonl).  NOC_PERSIST_WIDE=0|1 overrides.
 // (Re-packing the last <= #CUs trajectories of a large batch onto it was measured and dropped:
 // those are Newton retries, KKT-bound, and the wide KKT solve is no faster -- DESIGN.md §3.7.)
 static bool use_wide(const noc_family& p, const noc_ipm_ws& w) {
@@ -586,7 +590,7 @@ static bool use_wide(const noc_family& p, const noc_ipm_ws& w) {
   if (!ipm_wide_supported(p, w.N)) return false;
   if (env && atoi(env) == 1) return true;
   static const int cus = device_simds() / 4;
-  return cus > 0 && w.Bt <= cus;
+  return cus > 0 && w.Bt <= cus && w.N > 128;
 }
 
 hipError_t ipm_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal, double bp0,
