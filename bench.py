@@ -173,6 +173,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=512)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ipm", action="store_true", help="skip the end-to-end solve line")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch every step from Python instead of replaying a HIP graph of the "
+                         "K timed steps (small configs then measure the host's launch rate)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -220,8 +223,27 @@ def main():
         def step():
             lqt.kkt_solve(*nat, reg=blocks["reg"], lanes=lanes, out=out)
 
+    # The K timed steps are one HIP graph (captured once, replayed once): a c2-sized launch runs
+    # ~10 us, less than a Python + ctypes launch takes on the host, so eager launches would time
+    # the host.  The graph holds exactly K kernel launches on the same buffers.
+    graph = None
+    if not args.no_graph:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            step()  # allocator / library warm-up on the capture stream
+        torch.cuda.current_stream().wait_stream(side)
+        g1, graph = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1):
+            step()
+        with torch.cuda.graph(graph):
+            for _ in range(args.steps):
+                step()
     for _ in range(args.warmup):
-        step()
+        if graph is not None:
+            g1.replay()
+        else:
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -229,8 +251,11 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record()
-    for _ in range(args.steps):
-        step()
+    if graph is not None:
+        graph.replay()
+    else:
+        for _ in range(args.steps):
+            step()
     ev1.record()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -272,6 +297,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": abytes, "kernel_ms": kern_ms},
         "feasible_fraction": feasible_frac,
+        "launch": "eager" if graph is None else "hip_graph (the K timed steps captured once, one replay)",
     }
     if not args.no_ipm:
         result["ipm_solve"] = ipm_solve_rate(args.problem, N, B, rank, world)
