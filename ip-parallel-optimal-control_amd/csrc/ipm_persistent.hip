@@ -364,7 +364,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       }
       // ---------------- KKT solve (par_Newton, P:107-124) ----------------
 #ifndef NOC_EXPT_NOKKT
-      kkt_scan_wave<NX, NU, PL, false, true>(a, b, l);
+      kkt_scan_wave<NX, NU, PL, false, true, 0, false>(a, b, l);
 #endif
       wave_fence();  // pred / feasible written by lane 0
       {

@@ -431,7 +431,10 @@ struct ArgsSrc {
 // registers once, all loads issued up front, and phases 1, 3 and 4 read it from there -- one pass
 // over the blocks and one exposed memory latency instead of three dependent load chains (small
 // nx with one- or two-stage chunks, c2).
-template <int NX, int NU, int L, bool AFF, bool TILED, class SRC, int CACHE = 0>
+// HANDOFF: phase 3 hands the chunk's first stage (A, B) to phase 4 in registers (standalone
+// scan: −1 stage of phase 4's re-reads); off inside the persistent solver, whose register budget
+// it would push into scratch (444 -> 516 B/lane).
+template <int NX, int NU, int L, bool AFF, bool TILED, class SRC, int CACHE = 0, bool HANDOFF = true>
 NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, const SRC& src) {
   constexpr int KD = kd_width<NX, NU>();
   if (traj >= a.B) return;                     // uniform over the segment
@@ -455,6 +458,12 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
 
   Mat<NX, NX> Phi;
   Vec<NX> phi;
+  // A, B (and c) of the chunk's first stage: phase 3 reads them last, phase 4 first -- handed over
+  // in registers instead of re-read (one stage of phase 4's A, B stream and its first exposed load)
+  Mat<NX, NX> hA;
+  Mat<NX, NU> hB;
+  Vec<NX> hc;
+  bool handed = false;
   // ablation bit 4 (timing only, results wrong): phases 3 and 4 re-read the blocks of trajectory
   // traj & 1 instead of their own -- an L2-resident working set, so the time they lose against
   // the full kernel is the cost of re-reading the blocks from beyond L2
@@ -627,10 +636,27 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       // not software pipelined: prefetching stage s-1 during stage s (registers) was measured
       // slower (phase 3 44k -> 60k cycles per wave at c3: the prefetch spills, and the phase runs
       // at the memory-side-cache rate, not at a per-stage latency, tools/scan_stamps.py)
-      for (int s = start + len - 1; s >= start; --s) {
-        StageData<NX, NU> st;
-        src_re.stage(s, s - start, reg, st);
-        riccati_stage(s, st);
+      if constexpr (HANDOFF) {
+        for (int s = start + len - 1; s > start; --s) {
+          StageData<NX, NU> st;
+          src_re.stage(s, s - start, reg, st);
+          riccati_stage(s, st);
+        }
+        if (len > 0) {  // the chunk's first stage, peeled: its A, B (c) go on to phase 4
+          StageData<NX, NU> st;
+          src_re.stage(start, 0, reg, st);
+          riccati_stage(start, st);
+          hA = st.A;
+          hB = st.B;
+          if constexpr (AFF) hc = st.c; else set_zero(hc);
+          handed = a.mode == MODE_FULL && !(a.ablate & 32);
+        }
+      } else {
+        for (int s = start + len - 1; s >= start; --s) {
+          StageData<NX, NU> st;
+          src_re.stage(s, s - start, reg, st);
+          riccati_stage(s, st);
+        }
       }
     }
     // segment reductions: pred = sum, feasible = and
@@ -783,7 +809,20 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   } else {
     // one stage prefetched (a two-deep prefetch measured no faster: the propagation runs at the
     // rate the A, B re-reads stream at, not at the per-stage latency)
-    if (len > 0) fetch(start);
+    if (len > 0) {
+      if (handed) {  // stage `start` from phase 3's registers; only its K, d from the LDS slot
+        nA = hA;
+        nB = hB;
+        nc = hc;
+        if (kd_lds) {
+          NOC_UNROLL for (int i = 0; i < NU * (NX + 1); ++i) nK[i] = slot[start * KD + i];
+        } else {
+          load_Kd<NX, NU, L, TILED>(a, traj, tN + start, 0, l, cmax, nK);
+        }
+      } else {
+        fetch(start);
+      }
+    }
     for (int s = start; s < start + len; ++s) {
       const Mat<NX, NX> A = nA;
       const Mat<NX, NU> Bm = nB;
@@ -834,11 +873,12 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   NOC_STAMP(6);
 }
 
-template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE = 0>
+template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE = 0, bool HANDOFF = true>
 NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
   const int cmax = a.N / L + (a.N % L ? 1 : 0);
   const ArgsSrc<NX, NU, L, AFF, TILED> src{a, traj, l, cmax, (size_t)traj * a.N};
-  kkt_scan_wave_src<NX, NU, L, AFF, TILED, ArgsSrc<NX, NU, L, AFF, TILED>, CACHE>(a, traj, l, src);
+  kkt_scan_wave_src<NX, NU, L, AFF, TILED, ArgsSrc<NX, NU, L, AFF, TILED>, CACHE, HANDOFF>(a, traj, l,
+                                                                                          src);
 }
 
 template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE>

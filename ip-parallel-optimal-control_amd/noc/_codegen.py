@@ -36,7 +36,7 @@ class _DevicePrinter(C99CodePrinter):
             return f"sqrt({self._print(b)})"
         if e == sp.Rational(-1, 2):
             return f"(1.0/sqrt({self._print(b)}))"
-        return super()._print_Pow(expr, rational=rational)
+        return super()._print_Pow(expr)
 
 
 def _ccode(e) -> str:
