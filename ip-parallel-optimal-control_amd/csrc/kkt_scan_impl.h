@@ -41,6 +41,12 @@
 #define NOC_SCAN_NT 1
 #endif
 
+// Phase 4's forward affine scan: 1 = Sklansky tree with VALU partner fetches (DPP / readlane),
+// 0 = Hillis-Steele with ds_bpermute shuffles
+#ifndef NOC_FWD_SKLANSKY
+#define NOC_FWD_SKLANSKY 1
+#endif
+
 namespace noc {
 
 // Diagnostic build only (-DNOC_SCAN_STAMPS, `make stamps-lib`): lane 0 of every wave of the
@@ -720,6 +726,9 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     }
     set_zero(Phi);
   }
+#if NOC_FWD_SKLANSKY
+  affine_prefix_sklansky<NX, L>(Phi, phi);  // partners on the VALU (small_linalg.h)
+#else
 #pragma unroll 1
   for (int d = 1; d < L; d <<= 1) {
     Mat<NX, NX> oP;
@@ -741,6 +750,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     }
     Phi = Pn;
   }
+#endif
   Vec<NX> x;
   shfl_up_arr<NX>(phi.v, x.v, 1, L);
   if (l == 0) x = x0;

@@ -205,6 +205,82 @@ NOC_DEV void shfl_up_arr(const double* src, double* dst, int d, int w) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Sklansky (tree) inclusive prefix of affine maps x -> Phi x + phi over an L-lane segment, partners
+// fetched on the VALU instead of through the LDS pipe: at level k (h = 2^k) the upper half of every
+// aligned 2h-lane block composes with the last lane of its lower half -- a quad permutation
+// (k = 0, 1), a DPP row broadcast with bank masks (k = 2, 3) or a v_readlane (k = 4, 5: one source
+// lane per half-wave).  Non-combining lanes take the identity map as their partner, which leaves
+// them unchanged exactly.  Same result as the Hillis-Steele shfl_up scan up to association.
+template <int CTRL, int BANK>
+NOC_DEV double dpp_d(double old, double src) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(src), CTRL, 0xF, BANK, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(src), CTRL, 0xF, BANK, false);
+  return __hiloint2double(hi, lo);
+}
+NOC_DEV double readlane_dbl(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+// partner of lane `lane` at level K (idv for the lanes that do not combine at this level)
+template <int K>
+NOC_DEV double sklansky_fwd_partner(double v, double idv, int lane) {
+  if constexpr (K == 0) {
+    const double p = dpp_d<0xA0, 0xF>(v, v);  // quad_perm [0, 0, 2, 2]
+    return (lane & 1) ? p : idv;
+  } else if constexpr (K == 1) {
+    const double p = dpp_d<0x55, 0xF>(v, v);  // quad_perm [1, 1, 1, 1]
+    return (lane & 2) ? p : idv;
+  } else if constexpr (K == 2) {
+    const double p = dpp_d<0x153, 0x2>(idv, v);  // row_newbcast:3 -> lanes 4-7 of each row
+    return dpp_d<0x15B, 0x8>(p, v);              // row_newbcast:11 -> lanes 12-15
+  } else if constexpr (K == 3) {
+    return dpp_d<0x157, 0xC>(idv, v);  // row_newbcast:7 -> lanes 8-15
+  } else if constexpr (K == 4) {
+    const double a = readlane_dbl(v, 15), b = readlane_dbl(v, 47);
+    return (lane & 16) ? ((lane & 32) ? b : a) : idv;
+  } else {
+    const double a = readlane_dbl(v, 31);
+    return (lane & 32) ? a : idv;
+  }
+}
+template <int K, int NX, int L>
+NOC_DEV void sklansky_fwd_level(Mat<NX, NX>& Phi, Vec<NX>& phi, int lane) {
+  if constexpr ((1 << K) < L) {
+    Mat<NX, NX> oP;
+    Vec<NX> op;
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      NOC_UNROLL for (int j = 0; j < NX; ++j)
+        oP(i, j) = sklansky_fwd_partner<K>(Phi(i, j), i == j ? 1.0 : 0.0, lane);
+      op[i] = sklansky_fwd_partner<K>(phi[i], 0.0, lane);
+    }
+    Mat<NX, NX> Pn;
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      double t = phi[i];
+      NOC_UNROLL for (int k = 0; k < NX; ++k) t += Phi(i, k) * op[k];
+      phi[i] = t;
+      NOC_UNROLL for (int j = 0; j < NX; ++j) {
+        double u = 0.0;
+        NOC_UNROLL for (int k = 0; k < NX; ++k) u += Phi(i, k) * oP(k, j);
+        Pn(i, j) = u;
+      }
+    }
+    Phi = Pn;
+  }
+}
+template <int NX, int L>
+NOC_DEV void affine_prefix_sklansky(Mat<NX, NX>& Phi, Vec<NX>& phi) {
+  static_assert(L >= 1 && L <= 64 && (L & (L - 1)) == 0, "segment width: a power of two <= 64");
+  const int lane = (int)__lane_id();
+  sklansky_fwd_level<0, NX, L>(Phi, phi, lane);
+  sklansky_fwd_level<1, NX, L>(Phi, phi, lane);
+  sklansky_fwd_level<2, NX, L>(Phi, phi, lane);
+  sklansky_fwd_level<3, NX, L>(Phi, phi, lane);
+  sklansky_fwd_level<4, NX, L>(Phi, phi, lane);
+  sklansky_fwd_level<5, NX, L>(Phi, phi, lane);
+}
+
+// ---------------------------------------------------------------------------------------------
 // LDL' factorisation + solve of a small symmetric system (no pivoting).  Returns true iff the
 // matrix is positive definite (all D > 0, Sylvester), which is the eigh(Quu) > 0 test of
 // noc/seq_interior_point_newton.py:52-53.  Y (N x NR) is overwritten by W^{-1} Y.
