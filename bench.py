@@ -119,6 +119,7 @@ def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
     import torch
     import torch.distributed as dist
     from noc import problems
+    from noc import _lib
     from noc.ipm import BatchedIPM, persistent_supported
     ocp = problems.make_problem(problem, N)
     if not persistent_supported(ocp.family, N):
@@ -130,27 +131,45 @@ def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
     eng = BatchedIPM(ocp.family, N, B, persistent=True)
     eng.load(u0, x0)
     eng.solve(max_steps=8)  # warm-up
-    eng.load(u0, x0)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
-    eng.solve()
-    ev1.record()
-    torch.cuda.synchronize()
-    ms = ev0.elapsed_time(ev1)
+
+    def timed(flags):
+        eng.load(u0, x0)
+        eng.ws.flags = flags
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        eng.solve()
+        ev1.record()
+        torch.cuda.synchronize()
+        eng.ws.flags = 0
+        return ev0.elapsed_time(ev1)
+
+    # every retry recomputed (NOC_WS_NO_REPEAT_SKIP), then the default: the identical retries at
+    # the rp clip accounted without recomputation -- bit-identical results, checked here
+    ms_all = timed(_lib.WS_NO_REPEAT_SKIP)
+    U_all = eng.t["u"].clone()
+    ms = timed(0)
+    identical = bool(torch.equal(U_all, eng.t["u"]))
     U, its, solves = (t.cpu() for t in eng.result())
+    reps = eng.t["repeats"].cpu()
     done = int((eng.t["phase"] == 3).sum().item())
-    tot = [float(solves.sum()), float(done), float(its.double().sum()), float(B)]
-    mx = [ms, float(solves.max())]
+    tot = [float(solves.sum()), float(done), float(its.double().sum()), float(B),
+           float(reps.sum()), float(not identical)]
+    mx = [ms, float(solves.max()), ms_all]
     if world > 1:
         tot = allreduce(tot, "sum")
         mx = allreduce(mx, "max")
+    computed = tot[0] - tot[4]
     return {"what": "whole barrier schedule, noc_ipm_solve (one wave per trajectory, one launch "
                     "per rank)",
             "trajectories": int(tot[3]), "wall_ms": mx[0], "kkt_solves": int(tot[0]),
             "kkt_solves_per_s": tot[0] / (mx[0] * 1e-3),
+            "kkt_solves_computed": int(computed),
+            "repeats_accounted": int(tot[4]),
+            "wall_ms_recompute_all": mx[2],
+            "bit_identical_to_recompute_all": tot[5] == 0,
             "mean_newton_iters": tot[2] / max(tot[3], 1.0), "max_kkt_solves": int(mx[1]),
             "converged": int(tot[1])}
 

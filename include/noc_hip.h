@@ -156,6 +156,9 @@ typedef struct noc_family {
                               total_it, kkt_solves, x, u) at its phase -- ROLLOUT: a new barrier
                               stage, LINEARIZE: a new Newton iteration, SOLVE: a retry on the
                               current blocks, DONE: nothing -- instead of starting at bp0 */
+#define NOC_WS_NO_REPEAT_SKIP 4 /* flags bit: recompute every retry of the par inner loop, even the
+                              repeats at the rp clip that the solvers otherwise account without
+                              recomputing (ws->repeats; same results bit for bit either way) */
 typedef struct noc_ipm_ws {
   int Bt, N;
   int lanes;                           /* tiled layout of A,B,Q,R,M,r,K,d (8/16/32/64)  */
@@ -166,6 +169,9 @@ typedef struct noc_ipm_ws {
   double *dx, *du, *pred, *K, *d;      /* KKT outputs (dx, du natural; K, d tiled)  */
   int *feasible;                       /* (Bt) int32                               */
   int *phase, *kkt_active, *it, *inner, *total_it, *kkt_solves; /* (Bt) int32     */
+  int *repeats;                        /* (Bt) int32 or NULL: of kkt_solves, the retries that
+                                          repeat a rejected trial at the rp clip exactly and were
+                                          accounted without recomputation (par mode, P:151-188) */
   double *bp, *rp, *rinc, *cost, *hu, *gnorm, *reg;              /* (Bt)           */
 } noc_ipm_ws;
 

@@ -332,13 +332,18 @@ __global__ __launch_bounds__(256) void trial_kernel(noc_family prm, noc_ipm_ws w
   const double gain = (new_cost - cost) / pred;           // P:164-165
   const bool success = (gain > 0.0) && bwd_ok;            // P:166 / S:137
   double rp = w.rp[b], rinc = w.rinc[b];
+  const double rp_used = rp;
   const double shrink = fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0));
   rp = success ? rp * shrink : rp * rinc;                 // P:167-171 / S:139-143
   rinc = success ? 2.0 : 2.0 * rinc;                      // P:172 / S:144
   bool take, end_iter, stop;
-  int inner = w.inner[b] + 1;
+  int inner = w.inner[b] + 1, rep = 0;
   if (mode == NOC_MODE_PAR) {
     rp = fmin(fmax(rp, 1e-16), 1e16);                     // P:173
+    // identical retries at the rp clip: accounted, not recomputed (noc_internal.h)
+    rep = par_retry_repeats(w, success, rp_used, rp, inner, 501);
+    inner += rep;
+    rinc = ldexp(rinc, rep);                              // r_inc doubles per retry (P:172)
     end_iter = success || inner > 500;                    // P:177-182
     take = end_iter;                                      // the last trial is kept (P:175, P:184)
     stop = end_iter && (w.hu[b] < 1e-4 || w.it[b] + 1 > 1000);  // P:199-202
@@ -356,7 +361,8 @@ __global__ __launch_bounds__(256) void trial_kernel(noc_family prm, noc_ipm_ws w
     }
   }
   if (lane != 0) return;
-  w.kkt_solves[b] += 1;
+  w.kkt_solves[b] += 1 + rep;
+  if (w.repeats) w.repeats[b] += rep;
   w.inner[b] = inner;
   int it = w.it[b] + (end_iter ? 1 : 0);
   int phase;
@@ -394,6 +400,7 @@ __global__ __launch_bounds__(256) void init_kernel(noc_ipm_ws w, double bp0) {
   w.inner[b] = 0;
   w.total_it[b] = 0;
   w.kkt_solves[b] = 0;
+  if (w.repeats) w.repeats[b] = 0;
   w.bp[b] = bp0;
   w.rp[b] = 1.0;
   w.rinc[b] = 2.0;

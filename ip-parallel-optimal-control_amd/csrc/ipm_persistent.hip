@@ -108,6 +108,8 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
     gnorm = w.gnorm[b]; it = w.it[b]; inner = w.inner[b]; total_it = w.total_it[b];
     solves = w.kkt_solves[b]; entry = resume_phase(w.phase[b]);
     if (entry == NOC_PHASE_DONE) return;  // uniform over the wave
+  } else {
+    if (l == 0 && w.repeats) w.repeats[b] = 0;
   }
 
 #ifdef NOC_PERSIST_PROFILE
@@ -412,12 +414,21 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       const double gain = (new_cost - cost) / pred;             // P:164-165
       const bool success = (gain > 0.0) && bwd_ok;              // P:166 / S:137
       const double shrink = fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0));
+      const double rp_used = rp;
       rp = success ? rp * shrink : rp * rinc;                   // P:167-171 / S:139-143
       rinc = success ? 2.0 : 2.0 * rinc;                        // P:172 / S:144
       bool take, end_iter, stop;
       inner += 1;
       if (mode == NOC_MODE_PAR) {
         rp = fmin(fmax(rp, 1e-16), 1e16);                       // P:173
+        // identical retries at the rp clip: accounted, not recomputed (noc_internal.h)
+        const int rep = par_retry_repeats(w, success, rp_used, rp, inner, max_solves - solves - 1);
+        if (rep > 0) {
+          inner += rep;
+          solves += rep;
+          rinc = ldexp(rinc, rep);  // r_inc doubles per retry (P:172)
+          if (l == 0 && w.repeats) w.repeats[b] += rep;
+        }
         end_iter = success || inner > 500;                      // P:177-182
         take = end_iter;                                        // last trial kept (P:175, P:184)
         stop = end_iter && (hu < 1e-4 || it + 1 > 1000);        // P:199-202

@@ -228,6 +228,8 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
     bp = w.bp[b]; rp = w.rp[b]; rinc = w.rinc[b]; cost = w.cost[b]; hu = w.hu[b];
     gnorm = w.gnorm[b]; it = w.it[b]; inner = w.inner[b]; total_it = w.total_it[b];
     solves = w.kkt_solves[b]; phase = resume_phase(w.phase[b]);
+  } else if (t == 0 && w.repeats) {
+    w.repeats[b] = 0;
   }
   if (phase == NOC_PHASE_DONE) continue;  // uniform; no LDS written yet
   // resuming inside a barrier stage: the states are the workspace's (the blocks are recomputed
@@ -448,10 +450,22 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
       NOC_WSUB(0);
       // phase 2: in-wave reverse Hillis-Steele (the last wave's elements end at the terminal
       // cost, so its last level is value-only), then the waves joined through LDS
+#if NOC_REV_SKLANSKY
+      // reverse Sklansky, partners on the VALU; the upper half of every level combines with the
+      // identity, so a wave whose last lane does not end at the terminal cost needs no padding
+      combine_shfl<NX, false, false, 0>(e, 0, 64);
+      combine_shfl<NX, false, false, 1>(e, 0, 64);
+      combine_shfl<NX, false, false, 2>(e, 0, 64);
+      combine_shfl<NX, false, false, 3>(e, 0, 64);
+      combine_shfl<NX, false, false, 4>(e, 0, 64);
+      if (wv == W - 1) combine_shfl<NX, true, false, 5>(e, 0, 64);  // wave-uniform branch
+      else combine_shfl<NX, false, false, 5>(e, 0, 64);
+#else
 #pragma unroll 1
       for (int d = 1; d < 32; d <<= 1) combine_shfl<NX, false, true>(e, d, 64);
       if (wv == W - 1) combine_shfl<NX, true, true>(e, 32, 64);  // wave-uniform branch
       else combine_shfl<NX, false, true>(e, 32, 64);
+#endif
       NOC_WSUB(1);
       __syncthreads();  // the aggregate slots were last read by the costate phase
       if (l == 0) elem_put<NX>(sagg + wv * 64, e);
@@ -702,12 +716,21 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
       const double gain = (new_cost - cost) / pred;             // P:164-165
       const bool success = (gain > 0.0) && bwd_ok;              // P:166 / S:137
       const double shrink = fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0));
+      const double rp_used = rp;
       rp = success ? rp * shrink : rp * rinc;                   // P:167-171 / S:139-143
       rinc = success ? 2.0 : 2.0 * rinc;                        // P:172 / S:144
       bool take, end_iter, stop;
       inner += 1;
       if (mode == NOC_MODE_PAR) {
         rp = fmin(fmax(rp, 1e-16), 1e16);                       // P:173
+        // identical retries at the rp clip: accounted, not recomputed (noc_internal.h)
+        const int rep = par_retry_repeats(w, success, rp_used, rp, inner, max_solves - solves - 1);
+        if (rep > 0) {
+          inner += rep;
+          solves += rep;
+          rinc = ldexp(rinc, rep);  // r_inc doubles per retry (P:172)
+          if (t == 0 && w.repeats) w.repeats[b] += rep;
+        }
         end_iter = success || inner > 500;                      // P:177-182
         take = end_iter;                                        // last trial kept (P:175, P:184)
         stop = end_iter && (hu < 1e-4 || it + 1 > 1000);        // P:199-202

@@ -46,6 +46,11 @@
 #ifndef NOC_FWD_SKLANSKY
 #define NOC_FWD_SKLANSKY 1
 #endif
+// Phase 2's reverse scan of chunk elements: 1 = Sklansky tree with VALU partner fetches
+// (small_linalg.h: sklansky_rev_partner), 0 = Hillis-Steele with ds_bpermute shuffles
+#ifndef NOC_REV_SKLANSKY
+#define NOC_REV_SKLANSKY 1
+#endif
 
 namespace noc {
 
@@ -291,17 +296,26 @@ NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st, double reg) {
 // PAD_IDENTITY: partner-less lanes combine with the identity element (A = I, b = C = nu = J = 0)
 // instead of themselves, which leaves them unchanged exactly -- for segments whose last lane does
 // NOT end at the terminal cost (the waves of a multi-wave trajectory, ipm_wide.hip).
-template <int NX, bool VALUE_ONLY, bool PAD_IDENTITY = false>
+// SK >= 0: level SK of the reverse Sklansky scan instead (d, L unused): lanes whose bit SK is clear
+// combine with the first lane of the upper half of their aligned 2^(SK+1)-lane block, fetched on
+// the VALU (sklansky_rev_partner); the other lanes combine with the exact identity element.
+template <int NX, bool VALUE_ONLY, bool PAD_IDENTITY = false, int SK = -1>
 NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
   Sym<NX> J2;
   Vec<NX> nu2;
-  const bool pad = PAD_IDENTITY && (int)(__lane_id() % L) + d >= L;
+  const int lane = (int)__lane_id();
+  const bool pad = SK < 0 && PAD_IDENTITY && (lane % L) + d >= L;
   auto fetch_value = [&]() {
-    shfl_down_arr<Sym<NX>::SZ>(e1.J.v, J2.v, d, L);
-    shfl_down_arr<NX>(e1.nu.v, nu2.v, d, L);
-    if (pad) {
-      set_zero(J2);
-      set_zero(nu2);
+    if constexpr (SK >= 0) {
+      NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) J2.v[i] = sklansky_rev_partner<SK>(e1.J.v[i], 0.0, lane);
+      NOC_UNROLL for (int i = 0; i < NX; ++i) nu2.v[i] = sklansky_rev_partner<SK>(e1.nu.v[i], 0.0, lane);
+    } else {
+      shfl_down_arr<Sym<NX>::SZ>(e1.J.v, J2.v, d, L);
+      shfl_down_arr<NX>(e1.nu.v, nu2.v, d, L);
+      if (pad) {
+        set_zero(J2);
+        set_zero(nu2);
+      }
     }
   };
   fetch_value();
@@ -367,13 +381,21 @@ NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
     Mat<NX, NX> A2;
     Vec<NX> b2;
     Sym<NX> C2;
-    shfl_down_arr<NX * NX>(e1.A.v, A2.v, d, L);
-    shfl_down_arr<NX>(e1.b.v, b2.v, d, L);
-    shfl_down_arr<Sym<NX>::SZ>(e1.C.v, C2.v, d, L);
-    if (pad) {
-      set_identity(A2);
-      set_zero(b2);
-      set_zero(C2);
+    if constexpr (SK >= 0) {
+      NOC_UNROLL for (int i = 0; i < NX; ++i)
+        NOC_UNROLL for (int j = 0; j < NX; ++j)
+          A2(i, j) = sklansky_rev_partner<SK>(e1.A(i, j), i == j ? 1.0 : 0.0, lane);
+      NOC_UNROLL for (int i = 0; i < NX; ++i) b2.v[i] = sklansky_rev_partner<SK>(e1.b.v[i], 0.0, lane);
+      NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) C2.v[i] = sklansky_rev_partner<SK>(e1.C.v[i], 0.0, lane);
+    } else {
+      shfl_down_arr<NX * NX>(e1.A.v, A2.v, d, L);
+      shfl_down_arr<NX>(e1.b.v, b2.v, d, L);
+      shfl_down_arr<Sym<NX>::SZ>(e1.C.v, C2.v, d, L);
+      if (pad) {
+        set_identity(A2);
+        set_zero(b2);
+        set_zero(C2);
+      }
     }
     // A = A2 TA ; b = A2 Tb + b2 ; C = A2 TC A2' + C2
     Mat<NX, NX> T2;  // A2 * TC
@@ -397,6 +419,18 @@ NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
         NOC_UNROLL for (int k = 0; k < NX; ++k) s += T2(i, k) * A2(j, k);
         e1.C(i, j) = s;
       }
+  }
+}
+
+// Phase 2 as a reverse Sklansky scan over an L-lane segment: log2(L) levels, partners on the VALU;
+// the last level's partner (lane L/2 of the segment) covers the terminal cost -> value-only.
+template <int NX, int L, int K = 0>
+NOC_DEV void rev_scan_sklansky(Elem<NX>& e) {
+  if constexpr ((2 << K) < L) {
+    combine_shfl<NX, false, false, K>(e, 0, L);
+    rev_scan_sklansky<NX, L, K + 1>(e);
+  } else if constexpr ((2 << K) == L) {
+    combine_shfl<NX, true, false, K>(e, 0, L);
   }
 }
 
@@ -503,9 +537,13 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     NOC_STAMP(1);
     // ---------------- phase 2: reverse Hillis-Steele across lanes ----------------
     if (!(a.ablate & 1)) {
+#if NOC_REV_SKLANSKY
+      rev_scan_sklansky<NX, L>(e);
+#else
 #pragma unroll 1
       for (int d = 1; d < L / 2; d <<= 1) combine_shfl<NX, false>(e, d, L);
       combine_shfl<NX, true>(e, L / 2, L);  // last level: all right operands are value-only
+#endif
     }
     if (a.ablate & 4) {  // phase 1 (+2) only: keep the element alive, skip the rest
       if (a.pred) a.pred[traj] = e.J(0, 0) + e.A(0, 0) + e.C(0, 0) + e.nu[0] + e.b[0];

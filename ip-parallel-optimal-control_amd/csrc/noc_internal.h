@@ -40,6 +40,19 @@ inline size_t kkt_lds_bytes_rt(int nx, int nu, int N, int L) {
   return bytes <= 20480 ? bytes : 0;
 }
 
+// Retry fixed point of the par inner loop (P:151-188).  A rejected trial whose rp was already at
+// the upper clip (P:173: rp * r_inc clipped back to 1e16) leaves every input of the next par_Newton
+// call unchanged -- x, u, the LQ blocks, rp -- so every remaining retry of the iteration repeats
+// this trial bit for bit (deterministic kernels) until the retry cap keeps it (P:175-184).  Returns
+// how many of those identical retries to account for without recomputing them (each one: a KKT
+// solve, inner += 1, r_inc *= 2), at most `room` (a max_solves cap); 0 when the shortcut is off.
+__device__ __forceinline__ int par_retry_repeats(const noc_ipm_ws& w, bool success, double rp_used,
+                                                 double rp_new, int inner, int room) {
+  if ((w.flags & NOC_WS_NO_REPEAT_SKIP) || success || rp_new != rp_used || inner > 500) return 0;
+  const int k = 501 - inner;
+  return room < k ? (room > 0 ? room : 0) : k;
+}
+
 // standalone building blocks (derivatives.hip)
 struct DerivArgs {
   int N, B;

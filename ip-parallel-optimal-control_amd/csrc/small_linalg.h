@@ -244,6 +244,29 @@ NOC_DEV double sklansky_fwd_partner(double v, double idv, int lane) {
     return (lane & 32) ? a : idv;
   }
 }
+// Reverse (suffix) Sklansky: at level K (h = 2^K) the LOWER half of every aligned 2h-lane block
+// combines with the FIRST lane of its upper half; the upper half gets idv.
+template <int K>
+NOC_DEV double sklansky_rev_partner(double v, double idv, int lane) {
+  if constexpr (K == 0) {
+    const double p = dpp_d<0xF5, 0xF>(v, v);  // quad_perm [1, 1, 3, 3]
+    return (lane & 1) ? idv : p;
+  } else if constexpr (K == 1) {
+    const double p = dpp_d<0xAA, 0xF>(v, v);  // quad_perm [2, 2, 2, 2]
+    return (lane & 2) ? idv : p;
+  } else if constexpr (K == 2) {
+    const double p = dpp_d<0x154, 0x1>(idv, v);  // row_newbcast:4 -> lanes 0-3 of each row
+    return dpp_d<0x15C, 0x4>(p, v);              // row_newbcast:12 -> lanes 8-11
+  } else if constexpr (K == 3) {
+    return dpp_d<0x158, 0x3>(idv, v);  // row_newbcast:8 -> lanes 0-7
+  } else if constexpr (K == 4) {
+    const double a = readlane_dbl(v, 16), b = readlane_dbl(v, 48);
+    return (lane & 16) ? idv : ((lane & 32) ? b : a);
+  } else {
+    const double a = readlane_dbl(v, 32);
+    return (lane & 32) ? idv : a;
+  }
+}
 template <int K, int NX, int L>
 NOC_DEV void sklansky_fwd_level(Mat<NX, NX>& Phi, Vec<NX>& phi, int lane) {
   if constexpr ((1 << K) < L) {

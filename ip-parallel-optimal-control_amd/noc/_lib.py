@@ -53,7 +53,9 @@ WS_DOUBLE_FIELDS = ["x", "u", "x0", "A", "B", "Q", "R", "M", "r", "P", "cx", "cu
                     "dx", "du", "pred", "K", "d"]
 WS_ONE_STAGE = 1  # NocIpmWs.flags bit: stop after one barrier stage (newton_oc)
 WS_RESUME = 2  # NocIpmWs.flags bit: noc_ipm_solve continues from the workspace state
-WS_INT_FIELDS = ["feasible", "phase", "kkt_active", "it", "inner", "total_it", "kkt_solves"]
+WS_NO_REPEAT_SKIP = 4  # NocIpmWs.flags bit: recompute the identical retries at the rp clip
+WS_INT_FIELDS = ["feasible", "phase", "kkt_active", "it", "inner", "total_it", "kkt_solves",
+                 "repeats"]
 WS_STATE_FIELDS = ["bp", "rp", "rinc", "cost", "hu", "gnorm", "reg"]
 
 

@@ -228,7 +228,14 @@ def test_persistent_solve_respects_solve_cap(wide, monkeypatch):
 def test_wide_solve_matches_one_wave_kernel(name, N, Bt, mode, monkeypatch):
     """The wide whole-solve kernel (ipm_wide.hip: four waves per trajectory, blocks in LDS) against
     the one-wave kernel on the same inputs: identical outer iterations / KKT solves per trajectory,
-    controls within 1e-8 relative (the scans associate differently, so not bit-identical)."""
+    controls within 1e-8 relative (the scans associate differently, so not bit-identical).
+
+    One flip is tolerated, and only of one kind: at the convergence boundary the first trial of a
+    Newton iteration can be accepted by one association and rejected by the other; once rejected,
+    rp grows, the step shrinks to rounding size and every retry is rejected until the retry cap
+    (P:173-188) keeps the last trial -- exactly 500 extra KKT solves in the same outer iteration
+    count.  cartpole N=200 seed 33 trajectory 3 does this in the wide kernel (685 solves; the
+    one-wave kernel and the oracle: 185)."""
     from noc import problems, _lib
     from noc.ipm import BatchedIPM
     if name == "linear2":  # box-constrained double integrator (the LINEAR family's log barrier)
@@ -248,9 +255,14 @@ def test_wide_solve_matches_one_wave_kernel(name, N, Bt, mode, monkeypatch):
         torch.cuda.synchronize()
         res.append([t.cpu().numpy() for t in eng.result()] + [eng.t["phase"].cpu().numpy()])
     (Uw, itw, sw, phw), (Un, itn, sn, phn) = res
-    assert np.array_equal(itw, itn) and np.array_equal(sw, sn), (itw, itn, sw, sn)
+    assert np.array_equal(itw, itn), (itw, itn)
+    flip = sw != sn
+    assert flip.sum() <= 1 and np.all(np.abs(sw[flip] - sn[flip]) == 500), (sw, sn)
     assert np.all(phw == _lib.PHASE_DONE)
-    assert np.max(np.abs(Uw - Un)) <= 1e-8 * max(1.0, float(np.max(np.abs(Un))))
+    same = ~flip
+    assert np.max(np.abs(Uw[same] - Un[same])) <= 1e-8 * max(1.0, float(np.max(np.abs(Un))))
+    if flip.any():  # the kept trial is a rounding-size step: same optimum
+        assert np.max(np.abs(Uw[flip] - Un[flip])) <= 1e-6 * max(1.0, float(np.max(np.abs(Un))))
 
 
 def _resume_case(name, N, Bt, seed=5):
@@ -291,6 +303,41 @@ def test_capped_then_resumed_solve_equals_uninterrupted(name, N, Bt, mode, caps,
         a, b = eng.t[k].cpu().numpy(), ref.t[k].cpu().numpy()
         assert np.array_equal(a, b), (k, np.max(np.abs(a.astype(float) - b.astype(float))))
     assert np.all(eng.t["phase"].cpu().numpy() == _lib.PHASE_DONE)
+
+
+@pytest.mark.parametrize("wide", ["0", "1"])
+def test_retry_repeats_accounted_bit_identical(wide, monkeypatch):
+    """The identical retries at the rp clip (noc_internal.h par_retry_repeats: a rejected trial at
+    rp = 1e16 leaves every input of the next par_Newton call unchanged, so the rest of the retry
+    loop P:151-188 repeats it until the cap) are accounted without recomputation: same controls,
+    states and counters bit for bit as recomputing every retry (NOC_WS_NO_REPEAT_SKIP), also when
+    max_solves caps a solve inside such a run and NOC_WS_RESUME continues it."""
+    monkeypatch.setenv("NOC_PERSIST_WIDE", wide)
+    from noc import _lib
+    from noc.ipm import BatchedIPM
+    N, Bt = 200, 256
+    ocp, x0, u0 = _resume_case("cartpole", N, Bt, seed=11)
+    keys = ("u", "x", "kkt_solves", "total_it", "it", "inner", "phase", "bp", "rp", "rinc", "hu")
+
+    def run(flags, caps=()):
+        eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
+        eng.ws.flags = flags
+        eng.load(u0, x0)
+        for i, cap in enumerate(caps):
+            eng.solve_persistent(max_solves=cap, resume=i > 0)
+        eng.solve_persistent(resume=bool(caps))
+        torch.cuda.synchronize()
+        return {k: eng.t[k].cpu().numpy().copy() for k in keys + ("repeats",)}
+
+    full = run(_lib.WS_NO_REPEAT_SKIP)
+    skip = run(0)
+    capped = run(0, caps=(150, 300, 450, 600, 750))
+    assert full["repeats"].sum() == 0
+    assert skip["repeats"].sum() >= 400, skip["repeats"].sum()  # the batch has retry-cap runs
+    assert np.all(skip["phase"] == _lib.PHASE_DONE)
+    for k in keys:
+        assert np.array_equal(skip[k], full[k]), k
+        assert np.array_equal(capped[k], full[k]), k
 
 
 def test_linear8_ipm_uses_group_solve_and_is_exact():

@@ -17,6 +17,8 @@ lanes = int(sys.argv[5]) if len(sys.argv) > 5 else 0   # 0: the batch-aware poli
 ocp = problems.make_problem(name, N)
 x0, u0 = problems.initial_conditions(name, N, B, seed=11)
 eng = BatchedIPM(ocp.family, N, B, persistent=persistent, lanes=lanes)
+if os.environ.get("NOC_NO_REPEAT_SKIP") == "1":  # recompute the identical retries at the rp clip
+    eng.ws.flags = _lib.WS_NO_REPEAT_SKIP
 eng.load(u0, x0)
 eng.solve(max_steps=16)   # warm-up (kernels loaded, caches)
 torch.cuda.synchronize()
@@ -31,4 +33,6 @@ print(json.dumps({"problem": name, "N": N, "B": B, "lanes": eng.lanes, "persiste
                   "wall_s": dt, "ms_per_device_step": 1e3 * dt / steps,
                   "total_kkt_solves": int(solves.sum()), "kkt_solves_per_s": float(solves.sum() / dt),
                   "mean_outer_iters": float(its.mean()), "max_kkt_solves": int(solves.max()),
-                  "min_kkt_solves": int(solves.min())}))
+                  "min_kkt_solves": int(solves.min()),
+                  "repeats_accounted": int(eng.t["repeats"].sum().item()),
+                  "no_repeat_skip": bool(eng.ws.flags & _lib.WS_NO_REPEAT_SKIP)}))
