@@ -20,6 +20,7 @@
 // retry loop D:114-152, barrier loop D:189-208).  Layout: natural, per trajectory contiguous
 // (x (Bt, N+1, nx), u (Bt, N, nu)); workspace include/noc_hip.h noc_ddp_work_doubles.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include <cmath>
 
@@ -37,6 +38,7 @@ __device__ int g_ddp_trace_traj = 0;
 
 struct DdpArgs {
   int N, Bt, max_passes;
+  int skip_repeats;  // account the identical retries at the rp clip without recomputing them
   double bp0;
   const double* x0;
   double* u;
@@ -280,11 +282,22 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
         const double new_cost = ok ? tcost : INFINITY;             // D:121-125
         const double gain = (new_cost - cost) / pred;               // D:126-127
         success = (gain > 0.0) && feas;                             // D:128
+        const double rp_used = rp;
         rp = success ? rp * fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0))
                      : rp * reg_inc;                                // D:129-133: the OUTER reg_inc
         r_inc = success ? 2.0 : 2.0 * r_inc;                        // D:133
         rp = fmin(fmax(rp, 1e-16), 1e16);                           // D:135
         inner += 1;
+        // identical retries at the rp clip (the par rule, noc_internal.h par_retry_repeats): a
+        // rejected pass at rp = 1e16 leaves every input of the next pass unchanged (records, X, U,
+        // rp; reg_inc is the outer one), so the retries up to the cap repeat it bit for bit
+        if (a.skip_repeats && !g_ddp_trace && !success && rp == rp_used && inner <= 500) {
+          const int room = a.max_passes - passes;
+          const int k = (501 - inner) < room ? (501 - inner) : (room > 0 ? room : 0);
+          inner += k;
+          passes += k;
+          r_inc = ldexp(r_inc, k);  // D:133 per retry
+        }
         if (g_ddp_trace && lead && b < g_ddp_trace_traj && passes <= g_ddp_trace_cap) {
           // diagnostic trace (noc_debug_set_ddp_trace; off in product use): one record per pass
           double* tr = g_ddp_trace + ((size_t)b * g_ddp_trace_cap + (passes - 1)) * 10;
@@ -344,6 +357,8 @@ hipError_t ddp_solve(const noc_family& p, int N, int Bt, const double* x0, doubl
   a.N = N;
   a.Bt = Bt;
   a.max_passes = max_passes;
+  const char* no_skip = std::getenv("NOC_DDP_NO_REPEAT_SKIP");  // 1: recompute every retry
+  a.skip_repeats = !(no_skip && no_skip[0] == '1');
   a.bp0 = bp0;
   a.x0 = x0;
   a.u = u;

@@ -133,3 +133,36 @@ def test_ddp_single_trajectory_signature_and_cap():
     _, _, info = interior_point_ddp(ocp, u0, np.array([0.1, -0.1]), max_passes=5,
                                     return_info=True)
     assert not info["done"] and int(info["passes"]) == 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["linear", "cartpole"])
+def test_ddp_gpu_retry_repeats_accounted_bit_identical(case, monkeypatch):
+    """The identical retries at the rp clip (a rejected pass at rp = 1e16 leaves the next pass's
+    inputs unchanged, D:114-152) are accounted without recomputation: same controls, iterations
+    and pass counts bit for bit as recomputing them (NOC_DDP_NO_REPEAT_SKIP=1).  The LD problem
+    runs such a cap-length retry loop at its optimum (see the oracle test above); capping
+    max_passes inside it stops at exactly the same state."""
+    from noc import problems
+    from noc.differential_dynamic_programming import interior_point_ddp
+    if case == "linear":
+        N, Bt = 30, 3
+        ocp = problems.double_integrators(1, 0.1)
+        x0 = np.random.default_rng(4).normal(size=(Bt, 2))
+        u0 = np.zeros((Bt, N, 1))
+    else:
+        N, Bt = 40, 16
+        ocp = problems.make_problem("cartpole", N)
+        x0, u0 = problems.initial_conditions("cartpole", N, Bt, seed=7)
+    res = {}
+    for skip in ("0", "1"):
+        monkeypatch.setenv("NOC_DDP_NO_REPEAT_SKIP", "1" if skip == "0" else "0")
+        for cap in (10 ** 7, 250):
+            U, it, info = interior_point_ddp(ocp, u0, x0, max_passes=cap, return_info=True)
+            res[skip, cap] = (U, it, info["passes"], info["done"])
+    for cap in (10 ** 7, 250):
+        (Ua, ia, pa, da), (Ub, ib, pb, db) = res["0", cap], res["1", cap]
+        assert np.array_equal(Ua, Ub) and np.array_equal(ia, ib)
+        assert np.array_equal(pa, pb) and np.array_equal(da, db)
+    if case == "linear":
+        assert np.all(res["1", 10 ** 7][2] >= 501)  # a cap-length retry loop happened
