@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define NOC_ABI_VERSION 1
+#define NOC_ABI_VERSION 2 /* 2: noc_ipm_ws gained `repeats` */
 
 /* Library identity / diagnostics. */
 int noc_abi_version(void);

@@ -103,7 +103,7 @@ def _typed(lib: ctypes.CDLL) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.noc_abi_version() != 1:
+    if lib.noc_abi_version() != 2:
         raise NocError("libnoc_hip.so ABI version mismatch")
     return lib
 
