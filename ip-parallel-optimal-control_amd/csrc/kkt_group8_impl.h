@@ -12,7 +12,7 @@
 // 8 groups fall into different bank quarters (2-way instead of 8-way conflicts).
 // Contract of this path: Q and R are read through their upper triangle (lane q forms S_new[:, q]
 // from column q; the gathered S keeps entries i <= j), i.e. they are taken as symmetric.
-// The forward sweep keeps two stages of its row loads in flight in registers.
+// The forward sweep keeps NOC_G8_FWD_DEPTH stages of its row loads in flight in registers.
 // Two input layouts: natural (the ABI's [b][k][...]; each trajectory's 512/256/128 B blocks are
 // N*sz apart) and grouped (tiled with lanes = 1, small_linalg.h group_base: the wave's 8
 // trajectories of one stage contiguous per field, Q/R packed) -- what the IPM linearisation writes
@@ -71,6 +71,17 @@ NOC_DEV void glds16(const char* src, char* lds_dst) {
 #ifndef NOC_G8_DPP
 #define NOC_G8_DPP 1
 #endif
+// stages of the forward sweep's loads in flight per wave (fused kernel / forward-only launch)
+#ifndef NOC_G8_FWD_DEPTH
+#define NOC_G8_FWD_DEPTH 2
+#endif
+#ifndef NOC_G8_FWD_DEPTH_SPLIT
+#define NOC_G8_FWD_DEPTH_SPLIT 2
+#endif
+// 1: a full solve is a backward launch + a forward-only launch (see kkt_group8_kernel's FWD)
+#ifndef NOC_G8_SPLIT
+#define NOC_G8_SPLIT 0
+#endif
 // Broadcast lane J of every 8-lane group to the whole group on the VALU (DPP row_newbcast: lane n
 // of each 16-lane row to the row; bank_mask 0x3 writes lanes 0-7 of the row from row lane J, 0xC
 // lanes 8-15 from row lane 8+J) instead of a ds_bpermute through the LDS pipe, which the backward
@@ -103,7 +114,11 @@ NOC_DEV double gb(double x, int j) {
 }
 }  // namespace g8
 
-template <bool AFF, bool TILED>
+// FWD: the forward sweep alone, as its own launch after a MODE_BWD launch of the fused kernel
+// (launch_kkt_group8): its register budget is then its own, so its prefetch ring can be deeper
+// (NOC_G8_FWD_DEPTH_SPLIT stages instead of the fused kernel's NOC_G8_FWD_DEPTH, which the
+// backward sweep's 245 registers leave no room for).  K and d go through HBM either way.
+template <bool AFF, bool TILED, bool FWD = false>
 __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kernel(KKTArgs a) {
   using namespace g8;
   using LD = Lds<TILED>;
@@ -125,7 +140,9 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
   const size_t tN = (size_t)traj * N;
   const int trajc = traj < a.B ? traj : a.B - 1;  // clamped index for loads of tail groups
 
-  if (a.mode != MODE_FWD) {
+  // ablation bit 6 (timing only): skip the backward sweep, the forward sweep reads the K, d a
+  // previous full solve left in the output buffers (tools/kkt_ablate.py, lanes 1)
+  if (!FWD && a.mode != MODE_FWD && !(a.ablate & 64)) {
     // per-lane DMA source offsets (A and Q share theirs; the stage step is uniform)
     unsigned oA[4], oB[2], oQ[4];
     NOC_UNROLL for (int i = 0; i < 4; ++i) {
@@ -186,13 +203,20 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       const size_t mb = TILED ? group_base(NX * NU, N, trajc, s) : ((size_t)trajc * N + s) * (NX * NU);
       gload<NU>(a.M + mb + q * NU, m);
     };
+    // The M row is prefetched a stage ahead like the DMA and lands with it.  (Loaded at the top
+    // of its own stage, its first use waited vmcnt(0): the compiler does not count the LDS-DMA
+    // instructions issued next to it, so that wait also drained the next stage's DMA, which then
+    // overlapped only the first GEMVs of the stage instead of all of it.)
+    double mrow[NU], mnext[NU];
+    load_mrow(N - 1, mrow);
     issue(N - 1, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int s = N - 1; s >= 0; --s) {
       const int buf = (N - 1 - s) & 1;
-      if (s > 0) issue(s - 1, buf ^ 1);  // next stage streams in while this one is computed
-      double mrow[NU];
-      load_mrow(s, mrow);  // consumed after the S GEMVs below, which cover most of its latency
+      if (s > 0) {  // next stage streams in while this one is computed
+        load_mrow(s - 1, mnext);
+        issue(s - 1, buf ^ 1);
+      }
       const char* base = lds + buf * BUF;
       // row-rotated LDS images of trajectory g (see header)
       auto Arow = [&](int k) { return reinterpret_cast<const double*>(base + OA + g * 512 + ((k + g) & 7) * 64); };
@@ -296,16 +320,17 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       // stage s-1 has landed in the other buffer (and this stage's reads of `buf` are done
       // before the DMA after next overwrites it: the loads above were all consumed)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (s > 0) NOC_UNROLL for (int u = 0; u < NU; ++u) mrow[u] = mnext[u];
     }
     if (valid && q == 0) {
       if (a.pred) a.pred[traj] = pred;
       if (a.feasible) a.feasible[traj] = feas;
     }
-    if (a.mode == MODE_BWD) return;
+    if (a.mode == MODE_BWD || (a.ablate & 2)) return;  // ablation bit 1: no forward sweep
     __threadfence_block();  // this group's K, d stores are visible to its other lanes below
   }
 
-  // ---------------- forward rollout of the closed loop (two stages of loads in flight) --------
+  // ---------------- forward rollout of the closed loop (NOC_G8_FWD_DEPTH stages in flight) ----
   const size_t tNc = (size_t)trajc * N;
   Vec<NX> x;
   set_zero(x);
@@ -327,47 +352,79 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       cv = (AFF && a.c) ? a.c[si * NX + q] : 0.0;
     }
   };
-  double k0[NX], a0[NX], b0[NU], d0, c0, k1[NX], a1[NX], b1[NU], d1 = 0.0, c1 = 0.0;
-  load_f(0, k0, a0, b0, d0, c0);
-  if (N > 1) load_f(1, k1, a1, b1, d1, c1);
-  for (int s = 0; s < N; ++s) {
-    double kr[NX], ar[NX], br[NU];
-    NOC_UNROLL for (int i = 0; i < NX; ++i) { kr[i] = k0[i]; ar[i] = a0[i]; k0[i] = k1[i]; a0[i] = a1[i]; }
-    NOC_UNROLL for (int i = 0; i < NU; ++i) { br[i] = b0[i]; b0[i] = b1[i]; }
-    const double dv = d0, cv = c0;
-    d0 = d1;
-    c0 = c1;
-    if (s + 2 < N) load_f(s + 2, k1, a1, b1, d1, c1);
-    double uu = dv;
-    NOC_UNROLL for (int k = 0; k < NX; ++k) uu += kr[k] * x[k];
+  // Ring of NOC_G8_FWD_DEPTH stage buffers, the loop unrolled by the depth so every buffer has a
+  // fixed register home: stage s is computed from buffer s % DEPTH, which is then refilled with
+  // stage s + DEPTH.  (A rotating k0 <- k1 copy reads the prefetch registers and makes the
+  // compiler wait for the newest loads -- a vmcnt(0) per stage that left one stage of latency
+  // hiding: the forward sweep then ran at 4.4 TB/s, 2.19 ms of c4's 4.68.)
+  struct FwdStage {
+    double k[NX], a[NX], b[NU], d, c;
+  };
+  auto load_fs = [&](int s, FwdStage& f) { load_f(s, f.k, f.a, f.b, f.d, f.c); };
+  auto step_fs = [&](int s, const FwdStage& f) {
+    double uu = f.d;
+    NOC_UNROLL for (int k = 0; k < NX; ++k) uu += f.k[k] * x[k];
     double u[NU];
     NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = gb(uu, j);
-    double xn = cv;
-    NOC_UNROLL for (int k = 0; k < NX; ++k) xn += ar[k] * x[k];
-    NOC_UNROLL for (int j = 0; j < NU; ++j) xn += br[j] * u[j];
+    double xn = f.c;
+    NOC_UNROLL for (int k = 0; k < NX; ++k) xn += f.a[k] * x[k];
+    NOC_UNROLL for (int j = 0; j < NU; ++j) xn += f.b[j] * u[j];
     const size_t si = tN + s;
     if (valid && a.du && q < NU) a.du[si * NU + q] = uu;
     if (valid && a.dx) a.dx[(tN + traj + s + 1) * NX + q] = xn;
     NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = gb(xn, i);
+  };
+  // The refill loads are unconditional (stage index clamped to N - 1; the surplus reads are
+  // never used): a data-dependent skip would leave the compiler unsure how many memory ops follow
+  // a buffer's loads, and it then waits for all of them (vmcnt(0)) before every use.
+  constexpr int D = FWD ? NOC_G8_FWD_DEPTH_SPLIT : NOC_G8_FWD_DEPTH;
+  auto clamp_s = [&](int t) { return t < N ? t : N - 1; };
+  FwdStage fb[D];
+  NOC_UNROLL for (int j = 0; j < D; ++j) load_fs(clamp_s(j), fb[j]);
+  int s = 0;
+#pragma unroll 1
+  for (; s + D <= N; s += D) {
+    NOC_UNROLL for (int j = 0; j < D; ++j) {
+      step_fs(s + j, fb[j]);
+      load_fs(clamp_s(s + j + D), fb[j]);
+      // keep each refill after its own step: the scheduler hoisting later steps' loads above
+      // this point multiplies the live prefetch registers (spills at depth >= 3)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  NOC_UNROLL for (int j = 0; j < D; ++j)
+    if (s + j < N) step_fs(s + j, fb[j]);
+}
+
+template <bool FWD>
+static void launch_g8(const KKTArgs& a, unsigned grid, hipStream_t stream) {
+  using LN = g8::Lds<false>;
+  using LT = g8::Lds<true>;
+  const bool aff = a.q || a.c || a.p;
+  const size_t lds = FWD ? 0 : 2 * (a.tiled ? (aff ? LT::BUF_AFF : LT::BUF_PLAIN)
+                                            : (aff ? LN::BUF_AFF : LN::BUF_PLAIN));
+  if (a.tiled) {
+    if (aff) hipLaunchKernelGGL((kkt_group8_kernel<true, true, FWD>), dim3(grid), dim3(64), lds, stream, a);
+    else hipLaunchKernelGGL((kkt_group8_kernel<false, true, FWD>), dim3(grid), dim3(64), lds, stream, a);
+  } else {
+    if (aff) hipLaunchKernelGGL((kkt_group8_kernel<true, false, FWD>), dim3(grid), dim3(64), lds, stream, a);
+    else hipLaunchKernelGGL((kkt_group8_kernel<false, false, FWD>), dim3(grid), dim3(64), lds, stream, a);
   }
 }
 
 [[maybe_unused]] static hipError_t launch_kkt_group8(const KKTArgs& a, hipStream_t stream) {
   if (!a.K || !a.d) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.B + g8::TPW - 1) / g8::TPW);
-  const bool aff = a.q || a.c || a.p;
-  using LN = g8::Lds<false>;
-  using LT = g8::Lds<true>;
-  if (a.tiled) {
-    if (aff)
-      hipLaunchKernelGGL((kkt_group8_kernel<true, true>), dim3(grid), dim3(64), 2 * LT::BUF_AFF, stream, a);
-    else
-      hipLaunchKernelGGL((kkt_group8_kernel<false, true>), dim3(grid), dim3(64), 2 * LT::BUF_PLAIN, stream, a);
-  } else {
-    if (aff)
-      hipLaunchKernelGGL((kkt_group8_kernel<true, false>), dim3(grid), dim3(64), 2 * LN::BUF_AFF, stream, a);
-    else
-      hipLaunchKernelGGL((kkt_group8_kernel<false, false>), dim3(grid), dim3(64), 2 * LN::BUF_PLAIN, stream, a);
+  if (a.mode == MODE_FWD) {
+    launch_g8<true>(a, grid, stream);
+  } else if (a.mode == MODE_BWD || !NOC_G8_SPLIT) {
+    launch_g8<false>(a, grid, stream);
+  } else {  // full solve: backward launch, then the forward-only launch (ablation bits 1 / 6 drop one)
+    KKTArgs ab = a, af = a;
+    ab.mode = MODE_BWD;
+    af.mode = MODE_FWD;
+    if (!(a.ablate & 64)) launch_g8<false>(ab, grid, stream);
+    if (!(a.ablate & 2)) launch_g8<true>(af, grid, stream);
   }
   return hipGetLastError();
 }

@@ -14,9 +14,11 @@ lanes = int(sys.argv[4]) if len(sys.argv) > 4 else 64
 blk = problems.make_bench_blocks(name, N=N, batch=B, seed=7, lanes=lanes)
 tb = blk["tiled"]
 lib = _lib.load()
-out = lqt.kkt_solve_tiled(tb, reg=blk["reg"], want_gains=False)
+out = lqt.kkt_solve_tiled(tb, reg=blk["reg"], want_gains=(lanes == 1))
 variants = {"full": 0, "streamed": 8, "no_fwd": 2, "no_scan": 1, "no_scan_no_fwd": 3,
             "phase1_only": 5, "phase1+2": 4, "hot_rereads": 16}
+if lanes == 1:  # the group solve (kkt_group8_impl.h): backward sweep / forward sweep split
+    variants = {"full": 0, "no_fwd": 2, "fwd_only": 64}
 REPS = 10
 graphs = {}
 side = torch.cuda.Stream()
