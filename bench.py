@@ -132,7 +132,7 @@ def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
     eng.load(u0, x0)
     eng.solve(max_steps=8)  # warm-up
 
-    def timed(flags):
+    def timed(flags, schedule="auto"):
         eng.load(u0, x0)
         eng.ws.flags = flags
         torch.cuda.synchronize()
@@ -140,7 +140,7 @@ def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
             dist.barrier()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-        eng.solve()
+        eng.solve_persistent(schedule=schedule)  # incl. the launch-order pass (BatchedIPM)
         ev1.record()
         torch.cuda.synchronize()
         eng.ws.flags = 0
@@ -150,6 +150,7 @@ def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
     # the rp clip accounted without recomputation -- bit-identical results, checked here
     ms_all = timed(_lib.WS_NO_REPEAT_SKIP)
     U_all = eng.t["u"].clone()
+    ms_index = timed(0, "index")
     ms = timed(0)
     identical = bool(torch.equal(U_all, eng.t["u"]))
     U, its, solves = (t.cpu() for t in eng.result())
@@ -157,7 +158,7 @@ def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
     done = int((eng.t["phase"] == 3).sum().item())
     tot = [float(solves.sum()), float(done), float(its.double().sum()), float(B),
            float(reps.sum()), float(not identical)]
-    mx = [ms, float(solves.max()), ms_all]
+    mx = [ms, float(solves.max()), ms_all, ms_index]
     if world > 1:
         tot = allreduce(tot, "sum")
         mx = allreduce(mx, "max")
@@ -169,6 +170,9 @@ def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
             "kkt_solves_computed": int(computed),
             "repeats_accounted": int(tot[4]),
             "wall_ms_recompute_all": mx[2],
+            "wall_ms_index_order": mx[3],
+            "schedule": "descending initial cost when the batch exceeds the resident waves "
+                        "(BatchedIPM.launch_order, timed inside wall_ms)",
             "bit_identical_to_recompute_all": tot[5] == 0,
             "mean_newton_iters": tot[2] / max(tot[3], 1.0), "max_kkt_solves": int(mx[1]),
             "converged": int(tot[1])}

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define NOC_ABI_VERSION 2 /* 2: noc_ipm_ws gained `repeats` */
+#define NOC_ABI_VERSION 3 /* 2: noc_ipm_ws gained `repeats`; 3: `order` */
 
 /* Library identity / diagnostics. */
 int noc_abi_version(void);
@@ -172,6 +172,10 @@ typedef struct noc_ipm_ws {
   int *repeats;                        /* (Bt) int32 or NULL: of kkt_solves, the retries that
                                           repeat a rejected trial at the rp clip exactly and were
                                           accounted without recomputation (par mode, P:151-188) */
+  const int *order;                    /* (Bt) int32 or NULL: noc_ipm_solve's one-wave kernel
+                                          starts trajectory order[i] as its i-th workgroup (a
+                                          permutation of 0..Bt-1; results per trajectory are the
+                                          same for any order -- only the schedule changes) */
   double *bp, *rp, *rinc, *cost, *hu, *gnorm, *reg;              /* (Bt)           */
 } noc_ipm_ws;
 

@@ -68,7 +68,8 @@ template <int KIND, int NX, int NU, int WPS, bool RESUME>
 __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
                                                          int terminal, double bp0,
                                                          int max_solves) {
-  const int b = blockIdx.x;  // one wave (= one 64-thread workgroup) per trajectory
+  // one wave (= one 64-thread workgroup) per trajectory; w.order: the launch order (a permutation)
+  const int b = w.order ? w.order[blockIdx.x] : (int)blockIdx.x;
   const int l = threadIdx.x;
   if (b >= w.Bt) return;
   constexpr int KD = kd_width<NX, NU>();

@@ -59,10 +59,14 @@ WS_INT_FIELDS = ["feasible", "phase", "kkt_active", "it", "inner", "total_it", "
 WS_STATE_FIELDS = ["bp", "rp", "rinc", "cost", "hu", "gnorm", "reg"]
 
 
+WS_OPT_FIELDS = ["order"]  # optional pointers, NULL unless set (noc_ipm_ws.order)
+
+
 class NocIpmWs(ctypes.Structure):
     _fields_ = ([("Bt", _i), ("N", _i), ("lanes", _i), ("flags", _i)]
                 + [(f, _dp) for f in WS_DOUBLE_FIELDS]
-                + [(f, _dp) for f in WS_INT_FIELDS] + [(f, _dp) for f in WS_STATE_FIELDS])
+                + [(f, _dp) for f in WS_INT_FIELDS] + [(f, _dp) for f in WS_OPT_FIELDS]
+                + [(f, _dp) for f in WS_STATE_FIELDS])
 
 
 _fp = ctypes.POINTER(NocFamily)
@@ -103,7 +107,7 @@ def _typed(lib: ctypes.CDLL) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.noc_abi_version() != 2:
+    if lib.noc_abi_version() != 3:
         raise NocError("libnoc_hip.so ABI version mismatch")
     return lib
 

@@ -139,23 +139,48 @@ class BatchedIPM:
     def all_done(self) -> bool:
         return self.active_count() == 0
 
+    def _resident_slots(self) -> int:
+        """Trajectories the one-wave persistent kernel holds at once: 2 waves per SIMD."""
+        return 8 * torch.cuda.get_device_properties(self.device).multi_processor_count
+
+    def launch_order(self, mode: int, terminal: int, bp0: float) -> torch.Tensor:
+        """Highest initial cost first: the initial total cost (P:142 at bp0, one rollout +
+        linearisation, noc_ipm_prepare) is a cheap predictor of how many KKT solves a trajectory
+        needs; a batch larger than the resident waves then starts its expected stragglers first
+        instead of in index order (longest-processing-time-first list scheduling)."""
+        self.init(bp0)
+        self.prepare(mode, terminal)
+        return torch.argsort(self.t["cost"], descending=True, stable=True).to(torch.int32)
+
     def solve_persistent(self, mode: int = _lib.MODE_PAR, terminal: Optional[int] = None,
-                         bp0: float = 0.1, max_solves: int = 10 ** 7, resume: bool = False):
+                         bp0: float = 0.1, max_solves: int = 10 ** 7, resume: bool = False,
+                         schedule: str = "auto"):
         """The whole barrier schedule of every trajectory in ONE launch (noc_ipm_solve).
         Returns the KKT solves of the slowest trajectory (the multi-launch loop's step count).
         terminal=None: the reference's choice for the mode (par: XT = Q[0], P:73; seq: S:66).
         resume=True continues every trajectory from the workspace state a previous (capped)
-        solve left (NOC_WS_RESUME); max_solves counts the solves of both."""
+        solve left (NOC_WS_RESUME); max_solves counts the solves of both.
+        schedule: "index" launches trajectory i as workgroup i; "cost" launches them by
+        descending initial cost (launch_order, ws.order); "auto" = "cost" when the batch exceeds
+        the resident waves and this is not a resume.  Every trajectory's result is the same
+        either way (independent, deterministic); only the schedule changes."""
         terminal = default_terminal(mode) if terminal is None else terminal
+        if schedule not in ("auto", "cost", "index"):
+            raise ValueError(schedule)
+        ordered = not resume and (schedule == "cost" or (
+            schedule == "auto" and self.Bt > self._resident_slots()))
+        self._order = self.launch_order(mode, terminal, bp0) if ordered else None
         flags = self.ws.flags
         if resume:
             self.ws.flags = flags | _lib.WS_RESUME
+        self.ws.order = self._order.data_ptr() if ordered else None
         try:
             _lib.check(self._lib.noc_ipm_solve(ctypes.byref(self.fam_c), ctypes.byref(self.ws),
                                                mode, terminal, float(bp0), int(max_solves),
                                                self._stream()), "noc_ipm_solve", self._lib)
         finally:
             self.ws.flags = flags
+            self.ws.order = None
         return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
 
     def solve(self, mode: int = _lib.MODE_PAR, terminal: Optional[int] = None,

@@ -340,6 +340,28 @@ def test_retry_repeats_accounted_bit_identical(wide, monkeypatch):
         assert np.array_equal(capped[k], full[k]), k
 
 
+def test_cost_ordered_launch_gives_identical_results():
+    """noc_ipm_solve with a launch order (ws.order: descending initial cost, BatchedIPM
+    schedule="cost") only changes which trajectory starts when: every trajectory's controls,
+    states and counters are bit-identical to the index-order launch."""
+    from noc.ipm import BatchedIPM
+    N, Bt = 60, 96
+    ocp, x0, u0 = _resume_case("cartpole", N, Bt, seed=4)
+    keys = ("u", "x", "kkt_solves", "total_it", "phase", "bp", "rp", "rinc", "repeats")
+    res = {}
+    for sched in ("index", "cost"):
+        eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
+        eng.load(u0, x0)
+        if sched == "cost":
+            order = eng.launch_order(0, 1, 0.1).cpu().numpy()
+            assert sorted(order.tolist()) == list(range(Bt)) and order.tolist() != list(range(Bt))
+        eng.solve_persistent(schedule=sched)
+        torch.cuda.synchronize()
+        res[sched] = {k: eng.t[k].cpu().numpy().copy() for k in keys}
+    for k in keys:
+        assert np.array_equal(res["index"][k], res["cost"][k]), k
+
+
 def test_linear8_ipm_uses_group_solve_and_is_exact():
     """Four stacked double integrators (nx=8, nu=4; the c4 family): the IPM workspace defaults to
     the grouped layout + horizon-sequential group solve (lanes 1); the unconstrained LQ problem is

@@ -24,7 +24,7 @@ eng.solve(max_steps=16)   # warm-up (kernels loaded, caches)
 torch.cuda.synchronize()
 eng.load(u0, x0)
 t0 = time.perf_counter()
-steps = eng.solve()
+steps = eng.solve_persistent(schedule=os.environ.get("NOC_SCHEDULE", "auto")) if persistent else eng.solve()
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 U, its, solves = (t.cpu().numpy() for t in eng.result())
