@@ -11,7 +11,7 @@
 //   * phase 1  in-chunk element   : the lane folds its stages right-to-left into one scan element
 //                                  (A, b, C, nu, J) with the Riccati-form "prepend" (no R^-1);
 //                                  the segment's last lane starts from the terminal cost.
-//   * phase 2  cross-lane scan    : reverse Hillis-Steele over the L lanes, wave shuffles;
+//   * phase 2  cross-lane scan    : reverse Sklansky tree over the L lanes, DPP / readlane partners;
 //                                  afterwards lane l holds the value function at start_l.
 //   * phase 3  in-chunk Riccati   : from the true boundary value (lane l+1's result) the lane runs
 //                                  the sequential Riccati over its chunk -> gains K, d, value S, v,
@@ -50,6 +50,9 @@
 // (small_linalg.h: sklansky_rev_partner), 0 = Hillis-Steele with ds_bpermute shuffles
 #ifndef NOC_REV_SKLANSKY
 #define NOC_REV_SKLANSKY 1
+#endif
+#ifndef NOC_SEG_DPP
+#define NOC_SEG_DPP 1
 #endif
 
 namespace noc {
@@ -703,11 +706,16 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
         }
       }
     }
-    // segment reductions: pred = sum, feasible = and
+    // segment reductions: pred = sum, feasible = and (VALU butterfly, same association as the
+    // __shfl_xor loop it replaces -- NOC_SEG_DPP=0 keeps that loop)
+#if NOC_SEG_DPP
+    segment_sum_and<L>(pred, feas, (int)__lane_id());
+#else
     NOC_UNROLL for (int off = L / 2; off > 0; off >>= 1) {
       pred += __shfl_xor(pred, off, L);
       feas &= __shfl_xor(feas, off, L);
     }
+#endif
     if (l == 0) {
       if (a.pred) a.pred[traj] = pred;
       if (a.feasible) a.feasible[traj] = feas;

@@ -267,6 +267,43 @@ NOC_DEV double sklansky_rev_partner(double v, double idv, int lane) {
     return (lane & 32) ? idv : a;
   }
 }
+// Butterfly all-reduce over an L-lane segment on the VALU, bit-identical to the __shfl_xor loop
+// `for (off = L/2; off; off >>= 1) v = op(v, shfl_xor(v, off))`: the xor-32 / xor-16 partners
+// by v_permlane32_swap / v_permlane16_swap, xor-8 by row_ror:8, xor-4 by row_ror:12 (lane i <-
+// lane (i + 4) mod 16: the xor-4 partner for lanes 0-3 and 8-11 of a row, and its value for the
+// others once every value is symmetric under xor-8), xor-2 / xor-1 by quad_perm.  Lane 0 of every
+// segment -- the one whose result is used -- adds exactly the pairs of the shuffle loop.
+template <int CTRL>
+NOC_DEV int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+template <int OFF>
+NOC_DEV int xor_partner_i(int v, int lane) {
+  if constexpr (OFF == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (lane & 32) ? (int)r[0] : (int)r[1];
+  } else if constexpr (OFF == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane & 16) ? (int)r[0] : (int)r[1];
+  } else if constexpr (OFF == 8) {
+    return dpp_i<0x128>(v);  // row_ror:8
+  } else if constexpr (OFF == 4) {
+    return dpp_i<0x12C>(v);  // row_ror:12: lane i <- lane (i + 4) mod 16
+  } else if constexpr (OFF == 2) {
+    return dpp_i<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  } else {
+    return dpp_i<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  }
+}
+template <int L, int OFF = L / 2>
+NOC_DEV void segment_sum_and(double& sum, int& all, int lane) {
+  if constexpr (OFF >= 1) {
+    const int lo = xor_partner_i<OFF>(__double2loint(sum), lane);
+    const int hi = xor_partner_i<OFF>(__double2hiint(sum), lane);
+    sum += __hiloint2double(hi, lo);
+    all &= xor_partner_i<OFF>(all, lane);
+    segment_sum_and<L, OFF / 2>(sum, all, lane);
+  }
+}
+
 template <int K, int NX, int L>
 NOC_DEV void sklansky_fwd_level(Mat<NX, NX>& Phi, Vec<NX>& phi, int lane) {
   if constexpr ((1 << K) < L) {
