@@ -17,7 +17,10 @@ sequential Riccati (oracle/kkt_ref.c, OpenMP) on a bounded sample of the same bl
 N=1 only.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch G | --batch B]
-       (multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+Multi-GPU: `python bench.py --gpus N` starts N ranks itself (torch.distributed.run as a child
+process, before any GPU call in the parent, which only relays rank 0's line and exit code); under
+an external launcher (`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`) the
+ranks are the launcher's.  --gpus must equal the world size, else the bench refuses to run.
 """
 import argparse
 import json
@@ -41,15 +44,25 @@ def algorithmic_bytes(nx, nu, N, B):
     return B * N * per_stage + B * 8 * nx * nx
 
 
-def pmc_traffic(path, kernel_substr):
+def pmc_traffic(path, key):
     """HBM bytes per launch of the KKT kernel from a committed rocprofv3 --pmc summary (JSON written
-    by tools/pmc_traffic.py), or None."""
+    by tools/pmc_traffic.py) -- only if it was measured on THIS build of the KKT kernels (its
+    source_hash equals the current sources'), else None.  Returns (bytes or None, note)."""
+    from noc._lib import source_hash
     try:
         with open(path) as fh:
             d = json.load(fh)
-        return d.get(kernel_substr)
-    except Exception:
-        return None
+    except Exception as e:
+        return None, f"no PMC summary ({e!r})"
+    if key not in d:
+        return None, f"no PMC pass for {key} in {os.path.relpath(path, ROOT)}"
+    raw = d.get(key + "_raw", {})
+    cur = source_hash(raw.get("kernel_filter", "kkt_scan"))
+    if raw.get("source_hash") != cur:
+        return None, (f"stale: {key} was profiled on KKT sources {raw.get('source_hash')}, this "
+                      f"build is {cur} (re-run the FETCH_SIZE / WRITE_SIZE passes)")
+    return d[key], (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this build ({cur}), "
+                    f"{raw.get('correction', '')}")
 
 
 def cpu_baseline(blocks, sample, seconds=10.0, problem="cartpole"):
@@ -115,7 +128,9 @@ def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
     """End-to-end: the whole interior-point solve (P:228-254) of this rank's B trajectories with
     the persistent kernel (noc_ipm_solve, one launch), timed with HIP events; over ranks the wall
     time is the max and the solve counts are summed.  Reported beside the KKT metric:
-    trajectories x Newton KKT solves actually performed / wall time."""
+    kkt_solves_per_s = KKT solves actually COMPUTED / wall time (the identical retries at the rp
+    clip that are accounted without recomputation, ws.repeats, are excluded;
+    kkt_solves_reference_equivalent_per_s counts them as the reference would)."""
     import torch
     import torch.distributed as dist
     from noc import problems
@@ -166,8 +181,9 @@ def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
     return {"what": "whole barrier schedule, noc_ipm_solve (one wave per trajectory, one launch "
                     "per rank)",
             "trajectories": int(tot[3]), "wall_ms": mx[0], "kkt_solves": int(tot[0]),
-            "kkt_solves_per_s": tot[0] / (mx[0] * 1e-3),
+            "kkt_solves_per_s": computed / (mx[0] * 1e-3),
             "kkt_solves_computed": int(computed),
+            "kkt_solves_reference_equivalent_per_s": tot[0] / (mx[0] * 1e-3),
             "repeats_accounted": int(tot[4]),
             "wall_ms_recompute_all": mx[2],
             "wall_ms_index_order": mx[3],
@@ -176,6 +192,56 @@ def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
             "bit_identical_to_recompute_all": tot[5] == 0,
             "mean_newton_iters": tot[2] / max(tot[3], 1.0), "max_kkt_solves": int(mx[1]),
             "converged": int(tot[1])}
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus n` without a launcher: start n ranks (one process per GPU) with
+    torch.distributed.run as a CHILD process -- the parent has touched no GPU -- and return its
+    exit code.  Rank 0 prints the JSON line straight to the inherited stdout."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run_line(args, world, rank):
+    """NOC_BENCH_DRYRUN=1 (CPU tests): the launcher, process group, max-over-ranks timing and the
+    JSON assembly, with no GPU work -- value is null, so it can never pass for a measurement."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+    t = [0.0]
+    if world > 1:
+        t = allreduce(t, "max")
+        ranks = allgather_float(float(rank))
+    else:
+        ranks = [0.0]
+    return {"metric": "KKT Newton-steps/sec at (horizon N x batch)", "value": None,
+            "unit": "trajectory-KKT-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,
+            "dry_run": True, "data": "dry run: no GPU work (launcher / process-group rehearsal)",
+            "rccl_world_size": world, "ranks_seen": [int(r) for r in ranks]}
+
+
+def allgather_float(v):
+    """One fp64 scalar from every rank, in rank order (per-rank kernel times in the line)."""
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(o.item()) for o in out]
 
 
 def main():
@@ -201,23 +267,41 @@ def main():
                          "K timed steps (small configs then measure the host's launch rate)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
-
-    import torch
-    import torch.distributed as dist
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus must be >= 1 (got {args.gpus})")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: become one (nothing has touched the GPU in this process)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} "
+                 f"ranks; refusing to report a line whose n_gpus would not be what was asked")
+
+    import torch
+    import torch.distributed as dist
     # NOC_BENCH_REHEARSAL=1: every rank on cuda:0 over gloo -- rehearses the N > 1 code path on a
-    # one-GPU box (timings then share one GPU and mean nothing)
+    # one-GPU box (timings then share one GPU and mean nothing).  NOC_BENCH_DRYRUN=1: no GPU at all
+    # (CPU tests of the launcher / process group / JSON line; value null).
     rehearsal = os.environ.get("NOC_BENCH_REHEARSAL") == "1"
+    dry = os.environ.get("NOC_BENCH_DRYRUN") == "1"
     if rehearsal:
         local = 0
-    torch.cuda.set_device(local)
+    if not dry:
+        torch.cuda.set_device(local)
     if world > 1:
-        if rehearsal:
+        if rehearsal or dry:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if dry:
+        line = dry_run_line(args, world, rank)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     from noc import lqt, problems, _lib
 
     N = args.horizon
@@ -287,7 +371,9 @@ def main():
     torch.cuda.synchronize()
     kern_ms = ev0.elapsed_time(ev1) / args.steps          # HIP-event time per launch (stream)
     ms = wall * 1e3 / args.steps
+    rank_kern_ms = [kern_ms]
     if world > 1:
+        rank_kern_ms = allgather_float(kern_ms)
         ms, kern_ms = allreduce([ms, kern_ms], "max")
     feasible_frac = float(out.feasible.float().mean())
     value = G * args.steps / (ms * args.steps / 1e3)
@@ -295,7 +381,7 @@ def main():
     if world > 1:  # the slowest rank's bytes (shards differ by at most one trajectory)
         abytes = int(allreduce([abytes], "max")[0])
     achieved = abytes / (kern_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(args.pmc_json, f"{args.problem}_N{N}_B{B}")
+    traffic, traffic_note = pmc_traffic(args.pmc_json, f"{args.problem}_N{N}_B{B}")
     result = {
         "metric": "KKT Newton-steps/sec at (horizon N x batch)",
         "value": value,
@@ -318,7 +404,11 @@ def main():
                    "lanes_per_trajectory": lanes, "parallelism": f"trajectory-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_note": traffic_note,
                      "algorithmic_bytes_per_launch": abytes, "kernel_ms": kern_ms},
+        "rccl_world_size": dist.get_world_size() if world > 1 else 1,
+        "process_group": (dist.get_backend() if world > 1 else None),
+        "per_rank_kernel_ms": rank_kern_ms,
         "feasible_fraction": feasible_frac,
         "launch": "eager" if graph is None else "hip_graph (the K timed steps captured once, one replay)",
     }

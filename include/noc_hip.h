@@ -159,6 +159,7 @@ typedef struct noc_family {
 #define NOC_WS_NO_REPEAT_SKIP 4 /* flags bit: recompute every retry of the par inner loop, even the
                               repeats at the rp clip that the solvers otherwise account without
                               recomputing (ws->repeats; same results bit for bit either way) */
+/* Any other flags bit is rejected (-1) by every noc_ipm_* entry point. */
 typedef struct noc_ipm_ws {
   int Bt, N;
   int lanes;                           /* tiled layout of A,B,Q,R,M,r,K,d (8/16/32/64)  */
@@ -173,9 +174,14 @@ typedef struct noc_ipm_ws {
                                           repeat a rejected trial at the rp clip exactly and were
                                           accounted without recomputation (par mode, P:151-188) */
   const int *order;                    /* (Bt) int32 or NULL: noc_ipm_solve's one-wave kernel
-                                          starts trajectory order[i] as its i-th workgroup (a
-                                          permutation of 0..Bt-1; results per trajectory are the
-                                          same for any order -- only the schedule changes) */
+                                          starts trajectory order[i] as its i-th workgroup.  MUST
+                                          be a permutation of 0..Bt-1 (the caller's contract: the
+                                          library cannot check it without a device sync; an entry
+                                          outside 0..Bt-1 is skipped, a repeated one makes two
+                                          workgroups race on one trajectory).  Results per
+                                          trajectory are the same for any order -- only the
+                                          schedule changes.  The wide kernel (B <= #CUs) ignores it:
+                                          it runs one trajectory per CU at once anyway. */
   double *bp, *rp, *rinc, *cost, *hu, *gnorm, *reg;              /* (Bt)           */
 } noc_ipm_ws;
 

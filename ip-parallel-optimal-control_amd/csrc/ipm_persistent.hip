@@ -34,6 +34,8 @@ __device__ long long g_phase_cycles[8];
 // straggler that sets the wall time started and how its neighbours thinned out.
 constexpr int kTrajStamps = 16384;
 __device__ long long g_traj_times[kTrajStamps][2];
+// decision trace (-DNOC_DECISION_TRACE builds only; noc_internal.h)
+__device__ DecisionTrace g_dtrace;
 
 namespace {
 constexpr int PL = 64;  // lanes per trajectory in the persistent solver
@@ -71,7 +73,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
   // one wave (= one 64-thread workgroup) per trajectory; w.order: the launch order (a permutation)
   const int b = w.order ? w.order[blockIdx.x] : (int)blockIdx.x;
   const int l = threadIdx.x;
-  if (b >= w.Bt) return;
+  if (b < 0 || b >= w.Bt) return;  // an out-of-range order entry solves nothing (never faults)
   constexpr int KD = kd_width<NX, NU>();
   Fam<KIND, NX, NU> f(prm);
   const int N = w.N;
@@ -414,6 +416,10 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       const double new_cost = traj_ok ? tsum : INFINITY;       // P:159-163, S:126-129
       const double gain = (new_cost - cost) / pred;             // P:164-165
       const bool success = (gain > 0.0) && bwd_ok;              // P:166 / S:137
+#ifdef NOC_DECISION_TRACE
+      if (l == 0) NOC_TRACE_DECISION(g_dtrace, b, solves, bp, it, inner, cost, new_cost, pred, gain,
+                                     success, rp, rinc, hu, bwd_ok);
+#endif
       const double shrink = fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0));
       const double rp_used = rp;
       rp = success ? rp * shrink : rp * rinc;                   // P:167-171 / S:139-143
@@ -557,6 +563,19 @@ int debug_phase_cycles(long long* out, int n, int reset) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), zero, sizeof(zero)) != hipSuccess) return -1;
   }
   return 0;
+}
+
+// decision-trace buffer of both persistent kernels; 1 if this build records (NOC_DECISION_TRACE),
+// 0 if it has no trace code, -1 on a HIP error
+int debug_set_decision_trace(double* buf, int cap, int ntraj) {
+  const DecisionTrace t{buf, cap, ntraj};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_dtrace), &t, sizeof(t)) != hipSuccess) return -1;
+  if (wide_set_decision_trace(t) != 0) return -1;
+#ifdef NOC_DECISION_TRACE
+  return 1;
+#else
+  return 0;
+#endif
 }
 
 int debug_traj_times(long long* out, int n) {

@@ -9,8 +9,8 @@
 //   * the stage-parallel work (linearise P:13-28, the costate sweep C:34-54 fused with the LQ
 //     blocks P:31-42, the trial point P:156-175) is spread over 64 W lanes: one stage per lane up
 //     to N = 64 W instead of N / 64;
-//   * the KKT scan (par_Newton, P:107-124) keeps the in-wave reverse Hillis-Steele of the 64-lane
-//     scan (kkt_scan_impl.h: chunk element by Riccati-form prepend, combine_shfl) and joins the
+//   * the KKT scan (par_Newton, P:107-124) keeps the in-wave reverse Sklansky scan of the 64-lane
+//     scan (kkt_scan_impl.h: chunk element by Riccati-form prepend, combine_sklansky) and joins the
 //     W waves through LDS with value-only applications of the later waves' aggregates, so the
 //     dependent chain stays at six combine levels while each lane's chunk shrinks to one stage;
 //     the forward affine scan is joined the same way;
@@ -32,6 +32,8 @@ namespace noc {
 // noc_debug_phase_cycles with the one-wave kernel's): rollout, linearise, costate + blocks, KKT
 // scan, trial, number of Newton iterations.
 __device__ long long g_wide_cycles[16];
+// decision trace (-DNOC_DECISION_TRACE builds only; noc_internal.h)
+__device__ DecisionTrace g_wide_dtrace;
 #ifdef NOC_PERSIST_PROFILE
 #define NOC_WPHASE(i) do { const long long t_ = clock64(); if (b == 0 && t == 0) g_wide_cycles[i] += t_ - t_prev; t_prev = t_; } while (0)
 // sub-phases of the KKT solve (slots 8..15), timed by wave 0 lane 0 without moving t_prev
@@ -82,7 +84,7 @@ NOC_DEV void fput(double* base, int N, int s, const double* v) {
 }
 
 // e1 <- e1 (x) (value-only e2 = (J2, nu2)): the true value function at e1's start given the value
-// at its end (the VALUE_ONLY branch of combine_shfl with the partner given explicitly)
+// at its end (the VALUE_ONLY branch of combine_sklansky with the partner given explicitly)
 template <int NX>
 NOC_DEV void apply_value(Elem<NX>& e1, const Sym<NX>& J2, const Vec<NX>& nu2) {
   double X[NX][NX], Y[NX][NX];
@@ -108,9 +110,11 @@ NOC_DEV void apply_value(Elem<NX>& e1, const Sym<NX>& J2, const Vec<NX>& nu2) {
       J2A1(i, j) = s;
     }
   }
-  // every lane of the workgroup takes the same branch only within a wave: the fallback is
-  // per-lane (no shuffles here), so no uniformity is needed
-  if (!lu_np_solve<NX, NX>(X, Y)) {
+  // nx = 2: closed form (det(I + C1 J2) >= 1), as combine_sklansky; else the threshold-checked
+  // elimination with a per-lane fallback (no shuffles here, so no uniformity is needed)
+  if constexpr (NX == 2) {
+    solve2_closed<NX>(X, Y);
+  } else if (!lu_np_solve<NX, NX>(X, Y)) {
     build();
     lu_pp_solve<NX, NX>(X, Y);
   }
@@ -448,24 +452,17 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
         prepend<NX, NU, false>(e, st, reg);
       }
       NOC_WSUB(0);
-      // phase 2: in-wave reverse Hillis-Steele (the last wave's elements end at the terminal
-      // cost, so its last level is value-only), then the waves joined through LDS
-#if NOC_REV_SKLANSKY
-      // reverse Sklansky, partners on the VALU; the upper half of every level combines with the
-      // identity, so a wave whose last lane does not end at the terminal cost needs no padding
-      combine_shfl<NX, false, false, 0>(e, 0, 64);
-      combine_shfl<NX, false, false, 1>(e, 0, 64);
-      combine_shfl<NX, false, false, 2>(e, 0, 64);
-      combine_shfl<NX, false, false, 3>(e, 0, 64);
-      combine_shfl<NX, false, false, 4>(e, 0, 64);
-      if (wv == W - 1) combine_shfl<NX, true, false, 5>(e, 0, 64);  // wave-uniform branch
-      else combine_shfl<NX, false, false, 5>(e, 0, 64);
-#else
-#pragma unroll 1
-      for (int d = 1; d < 32; d <<= 1) combine_shfl<NX, false, true>(e, d, 64);
-      if (wv == W - 1) combine_shfl<NX, true, true>(e, 32, 64);  // wave-uniform branch
-      else combine_shfl<NX, false, true>(e, 32, 64);
-#endif
+      // phase 2: in-wave reverse Sklansky scan (the last wave's elements end at the terminal
+      // cost, so its last level is value-only), then the waves joined through LDS.  The upper
+      // half of every level keeps its element, so a wave whose last lane does not end at the
+      // terminal cost needs no padding.
+      combine_sklansky<NX, false, 0>(e);
+      combine_sklansky<NX, false, 1>(e);
+      combine_sklansky<NX, false, 2>(e);
+      combine_sklansky<NX, false, 3>(e);
+      combine_sklansky<NX, false, 4>(e);
+      if (wv == W - 1) combine_sklansky<NX, true, 5>(e);  // wave-uniform branch
+      else combine_sklansky<NX, false, 5>(e);
       NOC_WSUB(1);
       __syncthreads();  // the aggregate slots were last read by the costate phase
       if (l == 0) elem_put<NX>(sagg + wv * 64, e);
@@ -715,6 +712,10 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
       const double new_cost = traj_ok ? tr[0] : INFINITY;       // P:159-163, S:126-129
       const double gain = (new_cost - cost) / pred;             // P:164-165
       const bool success = (gain > 0.0) && bwd_ok;              // P:166 / S:137
+#ifdef NOC_DECISION_TRACE
+      if (t == 0) NOC_TRACE_DECISION(g_wide_dtrace, b, solves, bp, it, inner, cost, new_cost, pred,
+                                     gain, success, rp, rinc, hu, bwd_ok);
+#endif
       const double shrink = fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0));
       const double rp_used = rp;
       rp = success ? rp * shrink : rp * rinc;                   // P:167-171 / S:139-143
@@ -791,6 +792,10 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
   }
   __syncthreads();  // the next trajectory's controls overwrite the LDS read above
   }
+}
+
+int wide_set_decision_trace(const DecisionTrace& t) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_wide_dtrace), &t, sizeof(t)) == hipSuccess ? 0 : -1;
 }
 
 int debug_wide_cycles(long long* out, int n, int reset) {

@@ -1,0 +1,7 @@
+// Instantiation unit of the KKT scan for (nx, nu) = (8, 4), lanes 32 (see kkt_scan_8x4.hip).
+#include "kkt_scan_impl.h"
+
+namespace noc {
+template hipError_t launch_kkt<8, 4, 32, true>(const KKTArgs&, hipStream_t);
+template hipError_t launch_kkt<8, 4, 32, false>(const KKTArgs&, hipStream_t);
+}  // namespace noc

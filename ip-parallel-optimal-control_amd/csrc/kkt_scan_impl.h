@@ -37,23 +37,6 @@
 #define NOC_KKT_WAVES_PER_SIMD 2
 #endif
 
-#ifndef NOC_SCAN_NT
-#define NOC_SCAN_NT 1
-#endif
-
-// Phase 4's forward affine scan: 1 = Sklansky tree with VALU partner fetches (DPP / readlane),
-// 0 = Hillis-Steele with ds_bpermute shuffles
-#ifndef NOC_FWD_SKLANSKY
-#define NOC_FWD_SKLANSKY 1
-#endif
-// Phase 2's reverse scan of chunk elements: 1 = Sklansky tree with VALU partner fetches
-// (small_linalg.h: sklansky_rev_partner), 0 = Hillis-Steele with ds_bpermute shuffles
-#ifndef NOC_REV_SKLANSKY
-#define NOC_REV_SKLANSKY 1
-#endif
-#ifndef NOC_SEG_DPP
-#define NOC_SEG_DPP 1
-#endif
 
 namespace noc {
 
@@ -145,14 +128,9 @@ NOC_DEV void load_AB(const KKTArgs& a, int traj, size_t si, int j, int l, int cm
                      Mat<NX, NX>& A, Mat<NX, NU>& Bm, Vec<NX>& c) {
   set_zero(c);
   if constexpr (TILED) {
-#if NOC_SCAN_NT
-    // A, B are read for the last time here (phase 4 / the forward-mode map)
+    // A, B are read for the last time here (phase 4 / the forward-mode map): non-temporal
     tload_last<NX * NX, L>(a.A, traj, j, l, cmax, A.v);
     tload_last<NX * NU, L>(a.Bm, traj, j, l, cmax, Bm.v);
-#else
-    tload<NX * NX, L>(a.A, traj, j, l, cmax, A.v);
-    tload<NX * NU, L>(a.Bm, traj, j, l, cmax, Bm.v);
-#endif
     if constexpr (AFF) { if (a.c) tload<NX, L>(a.c, traj, j, l, cmax, c.v); }
   } else {
     gload<NX * NX>(a.A + si * (NX * NX), A.v);
@@ -288,44 +266,44 @@ NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st, double reg) {
   e.A = An;
 }
 
-// e1 <- e1 (x) e2  (e1 covers the earlier interval, e2 = the partner lane's element, later one).
-// Partner fields arrive by ds_bpermute in two batches so that at most one half of e2 is live at a
-// time.  Lanes without a partner (l + d >= L) receive their OWN element (__shfl_down width
-// semantics); such a lane already covers the suffix up to the terminal cost, so its element is
-// value-only (A = b = C = 0) and e (x) e == e exactly -- no selects, one uniform instruction
-// stream, and no shuffle ever reads an EXEC-masked lane.
+// e1 <- e1 (x) e2 at level SK of the reverse Sklansky scan over a segment (e1 covers the earlier
+// interval, e2 = the partner's element, the later one).  At level SK the lanes whose bit SK is
+// clear combine with the FIRST lane of the upper half of their aligned 2^(SK+1)-lane block; the
+// others keep e1 unchanged.  The partner's fields are fetched on the VALU (DPP / v_readlane,
+// small_linalg.h: sklansky_rev_fetch) at the segment's full EXEC -- a DPP source lane must be
+// active -- in two batches (J, nu first, then A, b, C) so that at most one half of e2 is live;
+// the arithmetic then runs under EXEC = the combining lanes only, so the lanes that keep their
+// element need neither an identity partner nor selects.
 // VALUE_ONLY: every right operand is value-only (the last level: partner l + L/2 covers the end),
-// so the result is value-only too and only J, nu are formed (T A1 is the only solve needed).
-// PAD_IDENTITY: partner-less lanes combine with the identity element (A = I, b = C = nu = J = 0)
-// instead of themselves, which leaves them unchanged exactly -- for segments whose last lane does
-// NOT end at the terminal cost (the waves of a multi-wave trajectory, ipm_wide.hip).
-// SK >= 0: level SK of the reverse Sklansky scan instead (d, L unused): lanes whose bit SK is clear
-// combine with the first lane of the upper half of their aligned 2^(SK+1)-lane block, fetched on
-// the VALU (sklansky_rev_partner); the other lanes combine with the exact identity element.
-template <int NX, bool VALUE_ONLY, bool PAD_IDENTITY = false, int SK = -1>
-NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
+// so the result is value-only too and only J, nu are formed (T A1 is the only solve needed); A, b,
+// C are zeroed in every lane.
+// T = (I + C1 J2)^-1: nx = 2 in closed form (one division; det(I + C1 J2) >= 1 for C1, J2 >= 0);
+// larger nx by threshold-checked Gaussian elimination without row exchanges, redone with partial
+// pivoting by the whole segment (uniform branch, so the re-fetch is legal) if any lane's check
+// fails.
+template <int NX, bool VALUE_ONLY, int SK>
+NOC_DEV void combine_sklansky(Elem<NX>& e1) {
+  const int lane = (int)__lane_id();
+  // MASKED: the arithmetic under EXEC = the combining lanes; else every lane computes, the others
+  // with the exact identity element as partner (which leaves them unchanged): nx = 4 elements
+  // are too large to keep old and new values apart across the branches without spilling
+  constexpr bool MASKED = NX <= 2;
+  const bool act = MASKED ? !(lane & (1 << SK)) : true;
+  const bool comb = !(lane & (1 << SK));
+  auto fetch = [&](double v, double idv) {
+    const double p = sklansky_rev_fetch<SK>(v, lane);
+    return MASKED ? p : (comb ? p : idv);
+  };
   Sym<NX> J2;
   Vec<NX> nu2;
-  const int lane = (int)__lane_id();
-  const bool pad = SK < 0 && PAD_IDENTITY && (lane % L) + d >= L;
   auto fetch_value = [&]() {
-    if constexpr (SK >= 0) {
-      NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) J2.v[i] = sklansky_rev_partner<SK>(e1.J.v[i], 0.0, lane);
-      NOC_UNROLL for (int i = 0; i < NX; ++i) nu2.v[i] = sklansky_rev_partner<SK>(e1.nu.v[i], 0.0, lane);
-    } else {
-      shfl_down_arr<Sym<NX>::SZ>(e1.J.v, J2.v, d, L);
-      shfl_down_arr<NX>(e1.nu.v, nu2.v, d, L);
-      if (pad) {
-        set_zero(J2);
-        set_zero(nu2);
-      }
-    }
+    NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) J2.v[i] = fetch(e1.J.v[i], 0.0);
+    NOC_UNROLL for (int i = 0; i < NX; ++i) nu2.v[i] = fetch(e1.nu.v[i], 0.0);
   };
-  fetch_value();
   constexpr int NR = VALUE_ONLY ? NX : 2 * NX + 1;
   double X[NX][NX];
   double Y[NX][NR];
-  auto build = [&]() {
+  auto build = [&]() {  // X = I + C1 J2,  Y = [A1 | b1 - C1 nu2 | C1]
     NOC_UNROLL for (int i = 0; i < NX; ++i) {
       NOC_UNROLL for (int j = 0; j < NX; ++j) {
         double s = (i == j) ? 1.0 : 0.0;
@@ -341,87 +319,83 @@ NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
       }
     }
   };
-  build();
+  fetch_value();
   //  J2A1 = J2 A1,  w = nu2 + J2 b1   (e1.A, e1.b are still the pre-combine values)
   Mat<NX, NX> J2A1;
   Vec<NX> w;
-  NOC_UNROLL for (int i = 0; i < NX; ++i) {
-    double sw = nu2[i];
-    NOC_UNROLL for (int k = 0; k < NX; ++k) sw += J2(i, k) * e1.b[k];
-    w[i] = sw;
-    NOC_UNROLL for (int j = 0; j < NX; ++j) {
-      double s = 0.0;
-      NOC_UNROLL for (int k = 0; k < NX; ++k) s += J2(i, k) * e1.A(k, j);
-      J2A1(i, j) = s;
-    }
-  }
-  // Y = [TA | Tb | TC],  T = (I + C1 J2)^-1: threshold-checked solve without row exchanges; if
-  // any lane's check fails the whole wave (uniform branch, so the re-shuffle is legal) redoes
-  // the solve with partial pivoting.  J2 / nu2 are re-fetched there instead of kept live.
-  const bool ok = lu_np_solve<NX, NR>(X, Y);
-  if (__any(!ok)) {
-    fetch_value();
+  bool ok = true;
+  if (act) {
     build();
-    lu_pp_solve<NX, NR>(X, Y);
-  }
-  // J = J1 + TA' J2 A1 ; nu = nu1 + TA' w
-  NOC_UNROLL for (int i = 0; i < NX; ++i) {
-    NOC_UNROLL for (int j = i; j < NX; ++j) {
-      double s = e1.J(i, j);
-      NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * J2A1(k, j);
-      e1.J(i, j) = s;
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      double sw = nu2[i];
+      NOC_UNROLL for (int k = 0; k < NX; ++k) sw += J2(i, k) * e1.b[k];
+      w[i] = sw;
+      NOC_UNROLL for (int j = 0; j < NX; ++j) {
+        double s = 0.0;
+        NOC_UNROLL for (int k = 0; k < NX; ++k) s += J2(i, k) * e1.A(k, j);
+        J2A1(i, j) = s;
+      }
     }
-    double s = e1.nu[i];
-    NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * w[k];
-    e1.nu[i] = s;
+    if constexpr (NX == 2) solve2_closed<NR>(X, Y);  // Y = [TA | Tb | TC]
+    else ok = lu_np_solve<NX, NR>(X, Y);
+  }
+  if constexpr (NX != 2) {
+    if (__any(!ok)) {  // uniform over the segment: J2 / nu2 re-fetched instead of kept live
+      fetch_value();
+      if (act) {
+        build();
+        lu_pp_solve<NX, NR>(X, Y);
+      }
+    }
+  }
+  if (act) {  // J = J1 + TA' J2 A1 ; nu = nu1 + TA' w
+    NOC_UNROLL for (int i = 0; i < NX; ++i) {
+      NOC_UNROLL for (int j = i; j < NX; ++j) {
+        double s = e1.J(i, j);
+        NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * J2A1(k, j);
+        e1.J(i, j) = s;
+      }
+      double s = e1.nu[i];
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * w[k];
+      e1.nu[i] = s;
+    }
   }
   if constexpr (VALUE_ONLY) {
     set_zero(e1.A);
     set_zero(e1.b);
     set_zero(e1.C);
   } else {
-    // second batch: partner's A, b, C (not yet modified by any lane at this level)
+    // second batch: the partner's A, b, C (no lane has modified them at this level)
     Mat<NX, NX> A2;
     Vec<NX> b2;
     Sym<NX> C2;
-    if constexpr (SK >= 0) {
-      NOC_UNROLL for (int i = 0; i < NX; ++i)
-        NOC_UNROLL for (int j = 0; j < NX; ++j)
-          A2(i, j) = sklansky_rev_partner<SK>(e1.A(i, j), i == j ? 1.0 : 0.0, lane);
-      NOC_UNROLL for (int i = 0; i < NX; ++i) b2.v[i] = sklansky_rev_partner<SK>(e1.b.v[i], 0.0, lane);
-      NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) C2.v[i] = sklansky_rev_partner<SK>(e1.C.v[i], 0.0, lane);
-    } else {
-      shfl_down_arr<NX * NX>(e1.A.v, A2.v, d, L);
-      shfl_down_arr<NX>(e1.b.v, b2.v, d, L);
-      shfl_down_arr<Sym<NX>::SZ>(e1.C.v, C2.v, d, L);
-      if (pad) {
-        set_identity(A2);
-        set_zero(b2);
-        set_zero(C2);
-      }
-    }
-    // A = A2 TA ; b = A2 Tb + b2 ; C = A2 TC A2' + C2
-    Mat<NX, NX> T2;  // A2 * TC
-    NOC_UNROLL for (int i = 0; i < NX; ++i) {
-      double sb = b2[i];
-      NOC_UNROLL for (int k = 0; k < NX; ++k) sb += A2(i, k) * Y[k][NX];
-      e1.b[i] = sb;
-      NOC_UNROLL for (int j = 0; j < NX; ++j) {
-        double sa = 0.0, st = 0.0;
-        NOC_UNROLL for (int k = 0; k < NX; ++k) {
-          sa += A2(i, k) * Y[k][j];
-          st += A2(i, k) * Y[k][NX + 1 + j];
-        }
-        e1.A(i, j) = sa;
-        T2(i, j) = st;
-      }
-    }
     NOC_UNROLL for (int i = 0; i < NX; ++i)
-      NOC_UNROLL for (int j = i; j < NX; ++j) {
-        double s = C2(i, j);
-        NOC_UNROLL for (int k = 0; k < NX; ++k) s += T2(i, k) * A2(j, k);
-        e1.C(i, j) = s;
+      NOC_UNROLL for (int j = 0; j < NX; ++j) A2(i, j) = fetch(e1.A(i, j), i == j ? 1.0 : 0.0);
+    NOC_UNROLL for (int i = 0; i < NX; ++i) b2.v[i] = fetch(e1.b.v[i], 0.0);
+    NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) C2.v[i] = fetch(e1.C.v[i], 0.0);
+    if (act) {  // A = A2 TA ; b = A2 Tb + b2 ; C = A2 TC A2' + C2
+      Mat<NX, NX> T2;  // A2 * TC
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        double sb = b2[i];
+        NOC_UNROLL for (int k = 0; k < NX; ++k) sb += A2(i, k) * Y[k][NX];
+        e1.b[i] = sb;
+        NOC_UNROLL for (int j = 0; j < NX; ++j) {
+          double sa = 0.0, st = 0.0;
+          NOC_UNROLL for (int k = 0; k < NX; ++k) {
+            sa += A2(i, k) * Y[k][j];
+            st += A2(i, k) * Y[k][NX + 1 + j];
+          }
+          e1.A(i, j) = sa;
+          T2(i, j) = st;
+        }
       }
+      NOC_UNROLL for (int i = 0; i < NX; ++i)
+        NOC_UNROLL for (int j = i; j < NX; ++j) {
+          double s = C2(i, j);
+          NOC_UNROLL for (int k = 0; k < NX; ++k) s += T2(i, k) * A2(j, k);
+          e1.C(i, j) = s;
+        }
+    }
   }
 }
 
@@ -429,11 +403,13 @@ NOC_DEV void combine_shfl(Elem<NX>& e1, int d, int L) {
 // the last level's partner (lane L/2 of the segment) covers the terminal cost -> value-only.
 template <int NX, int L, int K = 0>
 NOC_DEV void rev_scan_sklansky(Elem<NX>& e) {
+  NOC_ISA_MARK("rev", K);
   if constexpr ((2 << K) < L) {
-    combine_shfl<NX, false, false, K>(e, 0, L);
+    combine_sklansky<NX, false, K>(e);
     rev_scan_sklansky<NX, L, K + 1>(e);
   } else if constexpr ((2 << K) == L) {
-    combine_shfl<NX, true, false, K>(e, 0, L);
+    combine_sklansky<NX, true, K>(e);
+    NOC_ISA_MARK("rev", K + 1);
   }
 }
 
@@ -537,22 +513,16 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
         prepend<NX, NU, AFF>(e, st, reg);
       }
     }
-    NOC_STAMP(1);
-    // ---------------- phase 2: reverse Hillis-Steele across lanes ----------------
+    NOC_STAMP(1); NOC_ISA_MARK("phase", 1);
+    // ---------------- phase 2: reverse Sklansky scan across lanes ----------------
     if (!(a.ablate & 1)) {
-#if NOC_REV_SKLANSKY
       rev_scan_sklansky<NX, L>(e);
-#else
-#pragma unroll 1
-      for (int d = 1; d < L / 2; d <<= 1) combine_shfl<NX, false>(e, d, L);
-      combine_shfl<NX, true>(e, L / 2, L);  // last level: all right operands are value-only
-#endif
     }
     if (a.ablate & 4) {  // phase 1 (+2) only: keep the element alive, skip the rest
       if (a.pred) a.pred[traj] = e.J(0, 0) + e.A(0, 0) + e.C(0, 0) + e.nu[0] + e.b[0];
       return;
     }
-    NOC_STAMP(2);
+    NOC_STAMP(2); NOC_ISA_MARK("phase", 2);
     // ---------------- phase 3: in-chunk Riccati from the true boundary ----------------
     Sym<NX> S;
     Vec<NX> v;
@@ -706,21 +676,13 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
         }
       }
     }
-    // segment reductions: pred = sum, feasible = and (VALU butterfly, same association as the
-    // __shfl_xor loop it replaces -- NOC_SEG_DPP=0 keeps that loop)
-#if NOC_SEG_DPP
+    // segment reductions: pred = sum, feasible = and (VALU butterfly, small_linalg.h)
     segment_sum_and<L>(pred, feas, (int)__lane_id());
-#else
-    NOC_UNROLL for (int off = L / 2; off > 0; off >>= 1) {
-      pred += __shfl_xor(pred, off, L);
-      feas &= __shfl_xor(feas, off, L);
-    }
-#endif
     if (l == 0) {
       if (a.pred) a.pred[traj] = pred;
       if (a.feasible) a.feasible[traj] = feas;
     }
-    NOC_STAMP(3);
+    NOC_STAMP(3); NOC_ISA_MARK("phase", 3);
     if (a.mode == MODE_BWD || (a.ablate & 2)) return;
   } else {
     // MODE_FWD: gains are inputs; compose the chunk's closed-loop map from A, B, K, d
@@ -772,35 +734,11 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     }
     set_zero(Phi);
   }
-#if NOC_FWD_SKLANSKY
   affine_prefix_sklansky<NX, L>(Phi, phi);  // partners on the VALU (small_linalg.h)
-#else
-#pragma unroll 1
-  for (int d = 1; d < L; d <<= 1) {
-    Mat<NX, NX> oP;
-    Vec<NX> op;
-    shfl_up_arr<NX * NX>(Phi.v, oP.v, d, L);
-    shfl_up_arr<NX>(phi.v, op.v, d, L);
-    // lanes l < d get their own map back (__shfl_up width semantics); their prefix already starts
-    // at lane 0, whose map is constant (Phi = 0), so composing with it changes nothing.
-    Mat<NX, NX> Pn;
-    NOC_UNROLL for (int i = 0; i < NX; ++i) {
-      double t = phi[i];
-      NOC_UNROLL for (int k = 0; k < NX; ++k) t += Phi(i, k) * op[k];
-      phi[i] = t;
-      NOC_UNROLL for (int j = 0; j < NX; ++j) {
-        double u = 0.0;
-        NOC_UNROLL for (int k = 0; k < NX; ++k) u += Phi(i, k) * oP(k, j);
-        Pn(i, j) = u;
-      }
-    }
-    Phi = Pn;
-  }
-#endif
   Vec<NX> x;
   shfl_up_arr<NX>(phi.v, x.v, 1, L);
   if (l == 0) x = x0;
-  NOC_STAMP(4);
+  NOC_STAMP(4); NOC_ISA_MARK("phase", 4);
   // dx/du rows go through LDS (slot s of the trajectory's region holds K_s, d_s from phase 3 and
   // is overwritten by x_s, u_s here) and leave as whole contiguous rows: per-lane direct stores
   // would touch one cache line per lane per store instruction.
@@ -889,7 +827,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       fwd_stage(s, A, Bm, cc, Kk);
     }
   }
-  NOC_STAMP(5);
+  NOC_STAMP(5); NOC_ISA_MARK("phase", 5);
   if (!via_lds) {
     if (last && a.dx) gstore<NX>(a.dx + (tN + traj + N) * NX, x.v);
     return;
@@ -903,14 +841,10 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       double2* dst2 = reinterpret_cast<double2*>(dst);
       for (int i = l; i < (N + 1) * H; i += L) {
         const int s = i / H, e = 2 * (i - s * H);
-#if NOC_SCAN_NT
         noc_dbl2 v;
         v.x = slot[s * KD + e];
         v.y = slot[s * KD + e + 1];
         __builtin_nontemporal_store(v, reinterpret_cast<noc_dbl2*>(dst2 + i));
-#else
-        dst2[i] = make_double2(slot[s * KD + e], slot[s * KD + e + 1]);
-#endif
       }
     } else {
       for (int i = l; i < (N + 1) * NX; i += L) {
@@ -951,8 +885,10 @@ constexpr int kkt_cache_len() { return (NX <= 2 && L >= 32) ? 2 : 0; }
 
 
 // ---------------------------------------------------------------------------------------------
+// (not static: a shape whose instances take long to compile splits its lane counts over units,
+// kkt_scan_8x4*.hip, by explicit instantiation)
 template <int NX, int NU, int L, bool AFF>
-static hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
+hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
   KKTArgs a = a_in;
   const long long threads = (long long)a.B * L;
   const int block = 64;  // one wave per workgroup: waves are independent (no LDS sharing)

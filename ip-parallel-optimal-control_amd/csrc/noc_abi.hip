@@ -268,6 +268,9 @@ static int check_ipm(const noc_family* fam, const noc_ipm_ws* ws) {
                        ws->reg};
   for (const void* p : req)
     if (!p) return fail(-2, "a required workspace pointer is NULL");
+  if (ws->flags & ~(NOC_WS_ONE_STAGE | NOC_WS_RESUME | NOC_WS_NO_REPEAT_SKIP))
+    return fail(-1, "workspace flags: unknown bits set (NOC_WS_ONE_STAGE | NOC_WS_RESUME | "
+                    "NOC_WS_NO_REPEAT_SKIP are defined)");
   return 0;
 }
 
@@ -346,6 +349,15 @@ int noc_ipm_step_main(const noc_family* fam, const noc_ipm_ws* ws, int mode, int
 int noc_debug_phase_cycles(long long* out, int n, int reset) {
   if (!out || n < 0) return fail(-2, "out is NULL");
   return noc::debug_phase_cycles(out, n, reset) == 0 ? 0 : fail(-10, "hipMemcpyFromSymbol failed");
+}
+
+// Diagnostic export (not in include/noc_hip.h; tools/flip_probe.py): the decision-trace buffer of
+// the persistent solvers, (ntraj, cap, 12) doubles; NULL switches it off.  Returns 1 if this build
+// records (make trace-lib), 0 if it has no trace code.
+extern "C" int noc_debug_set_decision_trace(double* buf, int cap, int ntraj) {
+  if (cap < 0 || ntraj < 0) return fail(-1, "cap, ntraj must be >= 0");
+  const int rc = noc::debug_set_decision_trace(buf, cap, ntraj);
+  return rc < 0 ? fail(-10, "hipMemcpyToSymbol failed") : rc;
 }
 
 int noc_debug_traj_times(long long* out, int n) {

@@ -53,6 +53,30 @@ __device__ __forceinline__ int par_retry_repeats(const noc_ipm_ws& w, bool succe
   return room < k ? (room > 0 ? room : 0) : k;
 }
 
+// Diagnostic decision trace of the persistent interior-point solvers (built only with
+// -DNOC_DECISION_TRACE: `make trace-lib`, read by tools/flip_probe.py).  One record of
+// kTraceFields doubles per computed KKT solve of trajectories b < ntraj, indexed by the solve
+// count before the solve: bp, it, inner, cost, new_cost, pred, gain, success, rp, r_inc, |Hu|,
+// bwd feasible -- the inputs and the outcome of the accept test (P:159-173).  The product library
+// has no such code; noc_debug_set_decision_trace then returns 0.
+constexpr int kTraceFields = 12;
+struct DecisionTrace {
+  double* buf;
+  int cap, ntraj;
+};
+#define NOC_TRACE_DECISION(T, b, idx, bp, it, inner, cost, new_cost, pred, gain, success, rp,    \
+                           rinc, hu, bwd_ok)                                                      \
+  do {                                                                                          \
+    if ((T).buf && (b) < (T).ntraj && (idx) < (T).cap) {                                        \
+      double* r_ = (T).buf + ((size_t)(b) * (T).cap + (idx)) * kTraceFields;                    \
+      r_[0] = (bp); r_[1] = (it); r_[2] = (inner); r_[3] = (cost); r_[4] = (new_cost);           \
+      r_[5] = (pred); r_[6] = (gain); r_[7] = (success) ? 1.0 : 0.0; r_[8] = (rp);               \
+      r_[9] = (rinc); r_[10] = (hu); r_[11] = (bwd_ok) ? 1.0 : 0.0;                              \
+    }                                                                                           \
+  } while (0)
+int wide_set_decision_trace(const DecisionTrace& t);  // ipm_wide.hip's copy of the pointer
+int debug_set_decision_trace(double* buf, int cap, int ntraj);  // both kernels (ipm_persistent.hip)
+
 // standalone building blocks (derivatives.hip)
 struct DerivArgs {
   int N, B;

@@ -11,6 +11,14 @@ namespace noc {
 #define NOC_DEV __device__ __forceinline__
 #define NOC_UNROLL _Pragma("unroll")
 
+// ISA analysis builds only (-DNOC_ISA_MARKS, tools/isa_levels.py): an assembler comment at each
+// level / phase boundary of the scans, so per-level instruction counts can be read off the .s file
+#ifdef NOC_ISA_MARKS
+#define NOC_ISA_MARK(tag, k) asm volatile("; NOC_MARK " tag " %0" ::"i"(k))
+#else
+#define NOC_ISA_MARK(tag, k) do { } while (0)
+#endif
+
 template <int R, int C>
 struct Mat {
   double v[R * C];
@@ -205,16 +213,21 @@ NOC_DEV void shfl_up_arr(const double* src, double* dst, int d, int w) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Sklansky (tree) inclusive prefix of affine maps x -> Phi x + phi over an L-lane segment, partners
-// fetched on the VALU instead of through the LDS pipe: at level k (h = 2^k) the upper half of every
-// aligned 2h-lane block composes with the last lane of its lower half -- a quad permutation
-// (k = 0, 1), a DPP row broadcast with bank masks (k = 2, 3) or a v_readlane (k = 4, 5: one source
-// lane per half-wave).  Non-combining lanes take the identity map as their partner, which leaves
-// them unchanged exactly.  Same result as the Hillis-Steele shfl_up scan up to association.
+// Sklansky (tree) inclusive prefixes over an L-lane segment with partners fetched on the VALU
+// instead of through the LDS pipe (sklansky_*_fetch below; the scans: sklansky_fwd_level here,
+// kkt_scan_impl.h: combine_sklansky for the reverse scan of the KKT elements).
 template <int CTRL, int BANK>
 NOC_DEV double dpp_d(double old, double src) {
   const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(src), CTRL, 0xF, BANK, false);
   const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(src), CTRL, 0xF, BANK, false);
+  return __hiloint2double(hi, lo);
+}
+// DPP move with full row / bank masks (every lane is written, so no `old` operand: the compiler
+// needs no copy of a source that stays live)
+template <int CTRL>
+NOC_DEV double dpp_full(double src) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(src), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(src), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
 NOC_DEV double readlane_dbl(double v, int lane) {
@@ -222,49 +235,46 @@ NOC_DEV double readlane_dbl(double v, int lane) {
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
   return __hiloint2double(hi, lo);
 }
-// partner of lane `lane` at level K (idv for the lanes that do not combine at this level)
+// Partner fetches of the Sklansky scans for the lanes that combine at level K (h = 2^K); the
+// other lanes receive some other lane's value, which they must not use (they skip the level's
+// arithmetic under EXEC).  Run at the segment's full EXEC: a DPP source lane must be active.
+// Forward (prefix): the UPPER half of every aligned 2h-lane block reads the LAST lane of its lower
+// half -- quad permutations (K = 0, 1), DPP row broadcasts (K = 2, 3), v_readlane (K = 4, 5: one
+// source lane per half-wave).
 template <int K>
-NOC_DEV double sklansky_fwd_partner(double v, double idv, int lane) {
+NOC_DEV double sklansky_fwd_fetch(double v, int lane) {
   if constexpr (K == 0) {
-    const double p = dpp_d<0xA0, 0xF>(v, v);  // quad_perm [0, 0, 2, 2]
-    return (lane & 1) ? p : idv;
+    return dpp_full<0xA0>(v);                     // quad_perm [0, 0, 2, 2]
   } else if constexpr (K == 1) {
-    const double p = dpp_d<0x55, 0xF>(v, v);  // quad_perm [1, 1, 1, 1]
-    return (lane & 2) ? p : idv;
+    return dpp_full<0x55>(v);                     // quad_perm [1, 1, 1, 1]
   } else if constexpr (K == 2) {
-    const double p = dpp_d<0x153, 0x2>(idv, v);  // row_newbcast:3 -> lanes 4-7 of each row
-    return dpp_d<0x15B, 0x8>(p, v);              // row_newbcast:11 -> lanes 12-15
+    return dpp_d<0x15B, 0x8>(dpp_full<0x153>(v), v);  // row_newbcast:3, lanes 12-15 from :11
   } else if constexpr (K == 3) {
-    return dpp_d<0x157, 0xC>(idv, v);  // row_newbcast:7 -> lanes 8-15
+    return dpp_full<0x157>(v);                    // row_newbcast:7
   } else if constexpr (K == 4) {
     const double a = readlane_dbl(v, 15), b = readlane_dbl(v, 47);
-    return (lane & 16) ? ((lane & 32) ? b : a) : idv;
+    return (lane & 32) ? b : a;
   } else {
-    const double a = readlane_dbl(v, 31);
-    return (lane & 32) ? a : idv;
+    return readlane_dbl(v, 31);
   }
 }
-// Reverse (suffix) Sklansky: at level K (h = 2^K) the LOWER half of every aligned 2h-lane block
-// combines with the FIRST lane of its upper half; the upper half gets idv.
+// Reverse (suffix): the LOWER half of every aligned 2h-lane block reads the FIRST lane of its
+// upper half.
 template <int K>
-NOC_DEV double sklansky_rev_partner(double v, double idv, int lane) {
+NOC_DEV double sklansky_rev_fetch(double v, int lane) {
   if constexpr (K == 0) {
-    const double p = dpp_d<0xF5, 0xF>(v, v);  // quad_perm [1, 1, 3, 3]
-    return (lane & 1) ? idv : p;
+    return dpp_full<0xF5>(v);                     // quad_perm [1, 1, 3, 3]
   } else if constexpr (K == 1) {
-    const double p = dpp_d<0xAA, 0xF>(v, v);  // quad_perm [2, 2, 2, 2]
-    return (lane & 2) ? idv : p;
+    return dpp_full<0xAA>(v);                     // quad_perm [2, 2, 2, 2]
   } else if constexpr (K == 2) {
-    const double p = dpp_d<0x154, 0x1>(idv, v);  // row_newbcast:4 -> lanes 0-3 of each row
-    return dpp_d<0x15C, 0x4>(p, v);              // row_newbcast:12 -> lanes 8-11
+    return dpp_d<0x15C, 0x4>(dpp_full<0x154>(v), v);  // row_newbcast:4, lanes 8-11 from :12
   } else if constexpr (K == 3) {
-    return dpp_d<0x158, 0x3>(idv, v);  // row_newbcast:8 -> lanes 0-7
+    return dpp_full<0x158>(v);                    // row_newbcast:8
   } else if constexpr (K == 4) {
     const double a = readlane_dbl(v, 16), b = readlane_dbl(v, 48);
-    return (lane & 16) ? idv : ((lane & 32) ? b : a);
+    return (lane & 32) ? b : a;
   } else {
-    const double a = readlane_dbl(v, 32);
-    return (lane & 32) ? idv : a;
+    return readlane_dbl(v, 32);
   }
 }
 // Butterfly all-reduce over an L-lane segment on the VALU, bit-identical to the __shfl_xor loop
@@ -304,40 +314,59 @@ NOC_DEV void segment_sum_and(double& sum, int& all, int lane) {
   }
 }
 
+// Level K of the inclusive prefix of affine maps x -> Phi x + phi: the upper half of every aligned
+// 2^(K+1)-lane block composes its map with the lower half's last prefix (under EXEC: the other
+// lanes keep theirs exactly).
 template <int K, int NX, int L>
 NOC_DEV void sklansky_fwd_level(Mat<NX, NX>& Phi, Vec<NX>& phi, int lane) {
   if constexpr ((1 << K) < L) {
+    // MASKED (small nx): the composition runs under EXEC = the combining lanes; larger nx compose
+    // in every lane, the others with the identity map (fewer values live across a branch)
+    constexpr bool MASKED = NX <= 2;
+    const bool comb = (lane & (1 << K)) != 0;
     Mat<NX, NX> oP;
     Vec<NX> op;
     NOC_UNROLL for (int i = 0; i < NX; ++i) {
-      NOC_UNROLL for (int j = 0; j < NX; ++j)
-        oP(i, j) = sklansky_fwd_partner<K>(Phi(i, j), i == j ? 1.0 : 0.0, lane);
-      op[i] = sklansky_fwd_partner<K>(phi[i], 0.0, lane);
-    }
-    Mat<NX, NX> Pn;
-    NOC_UNROLL for (int i = 0; i < NX; ++i) {
-      double t = phi[i];
-      NOC_UNROLL for (int k = 0; k < NX; ++k) t += Phi(i, k) * op[k];
-      phi[i] = t;
       NOC_UNROLL for (int j = 0; j < NX; ++j) {
-        double u = 0.0;
-        NOC_UNROLL for (int k = 0; k < NX; ++k) u += Phi(i, k) * oP(k, j);
-        Pn(i, j) = u;
+        const double p = sklansky_fwd_fetch<K>(Phi(i, j), lane);
+        oP(i, j) = (MASKED || comb) ? p : (i == j ? 1.0 : 0.0);
       }
+      const double p = sklansky_fwd_fetch<K>(phi[i], lane);
+      op[i] = (MASKED || comb) ? p : 0.0;
     }
-    Phi = Pn;
+    if (!MASKED || comb) {
+      Mat<NX, NX> Pn;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) {
+        double t = phi[i];
+        NOC_UNROLL for (int k = 0; k < NX; ++k) t += Phi(i, k) * op[k];
+        phi[i] = t;
+        NOC_UNROLL for (int j = 0; j < NX; ++j) {
+          double u = 0.0;
+          NOC_UNROLL for (int k = 0; k < NX; ++k) u += Phi(i, k) * oP(k, j);
+          Pn(i, j) = u;
+        }
+      }
+      Phi = Pn;
+    }
   }
 }
 template <int NX, int L>
 NOC_DEV void affine_prefix_sklansky(Mat<NX, NX>& Phi, Vec<NX>& phi) {
   static_assert(L >= 1 && L <= 64 && (L & (L - 1)) == 0, "segment width: a power of two <= 64");
   const int lane = (int)__lane_id();
+  NOC_ISA_MARK("fwd", 0);
   sklansky_fwd_level<0, NX, L>(Phi, phi, lane);
+  NOC_ISA_MARK("fwd", 1);
   sklansky_fwd_level<1, NX, L>(Phi, phi, lane);
+  NOC_ISA_MARK("fwd", 2);
   sklansky_fwd_level<2, NX, L>(Phi, phi, lane);
+  NOC_ISA_MARK("fwd", 3);
   sklansky_fwd_level<3, NX, L>(Phi, phi, lane);
+  NOC_ISA_MARK("fwd", 4);
   sklansky_fwd_level<4, NX, L>(Phi, phi, lane);
+  NOC_ISA_MARK("fwd", 5);
   sklansky_fwd_level<5, NX, L>(Phi, phi, lane);
+  NOC_ISA_MARK("fwd", 6);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -452,6 +481,21 @@ NOC_DEV void lu_pp_solve(double (&X)[N][N], double (&Y)[N][NR]) {
       NOC_UNROLL for (int t = k + 1; t < N; ++t) s -= X[k][t] * Y[t][j];
       Y[k][j] = s * X[k][k];
     }
+  }
+}
+
+// Y <- X^{-1} Y for a 2 x 2 X in closed form: one division (the adjugate over det), no pivoting.
+// Used where det(X) is bounded away from 0 by construction (X = I + C J with C, J >= 0:
+// det = 1 + tr(CJ) + det(C) det(J) >= 1); Cramer's rule is forward stable for n = 2.
+template <int NR>
+NOC_DEV void solve2_closed(const double (&X)[2][2], double (&Y)[2][NR]) {
+  const double det = X[0][0] * X[1][1] - X[0][1] * X[1][0];
+  const double id = 1.0 / det;
+  const double a = X[1][1] * id, b = -X[0][1] * id, c = -X[1][0] * id, d = X[0][0] * id;
+  NOC_UNROLL for (int j = 0; j < NR; ++j) {
+    const double y0 = Y[0][j], y1 = Y[1][j];
+    Y[0][j] = a * y0 + b * y1;
+    Y[1][j] = c * y0 + d * y1;
   }
 }
 

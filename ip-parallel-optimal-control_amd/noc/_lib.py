@@ -13,6 +13,18 @@ from typing import Optional
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NOC_HIP_LIB", os.path.join(_HERE, "_lib", "libnoc_hip.so"))
 
+# sources the bench's KKT kernels (kkt_scan_kernel, kkt_group8_kernel) are compiled from: a
+# committed PMC traffic figure is valid only for the build it was measured on (source_hash)
+_COMMON_SOURCES = ("csrc/small_linalg.h", "csrc/noc_internal.h", "csrc/kkt_shapes.def", "Makefile",
+                   "../include/noc_hip.h")
+KKT_KERNEL_SOURCES = {
+    "kkt_scan": ("csrc/kkt_scan_impl.h", "csrc/kkt_scan_2x1.hip", "csrc/kkt_scan_4x1.hip",
+                 "csrc/kkt_scan_8x4.hip", "csrc/kkt_scan_8x4_l32.hip", "csrc/kkt_scan_8x4_l16.hip",
+                 "csrc/kkt_scan_8x4_l8.hip") + _COMMON_SOURCES,
+    "kkt_group8": ("csrc/kkt_group_impl.h", "csrc/kkt_group8_impl.h", "csrc/kkt_group.hip")
+    + _COMMON_SOURCES,
+}
+
 _dp = ctypes.c_void_p  # device pointers are passed as opaque addresses
 _i = ctypes.c_int
 
@@ -177,3 +189,15 @@ def require_device(t, name: str):
 def stream_handle(device=None) -> int:
     import torch
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def source_hash(kernel: str = "kkt_scan") -> str:
+    """sha256 (first 16 hex digits) of the sources a KKT kernel is compiled from
+    (KKT_KERNEL_SOURCES[kernel], relative to the package root)."""
+    import hashlib
+    pkg = os.path.dirname(_HERE)
+    h = hashlib.sha256()
+    for f in KKT_KERNEL_SOURCES[kernel]:
+        with open(os.path.join(pkg, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]

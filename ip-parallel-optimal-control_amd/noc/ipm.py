@@ -185,23 +185,26 @@ class BatchedIPM:
 
     def solve(self, mode: int = _lib.MODE_PAR, terminal: Optional[int] = None,
               bp0: float = 0.1, poll_every: int = 8, max_steps: Optional[int] = None):
-        """Run the barrier schedule to completion for every trajectory.  Returns the number of
-        device iterations (= KKT solves of the slowest trajectory).  terminal=None: the
-        reference's choice for the mode (par: XT = Q[0], P:73; seq: hessian(final_cost), S:66)."""
+        """Run the barrier schedule to completion for every trajectory.  Returns the KKT solves of
+        the slowest trajectory (kkt_solves.max(), on both paths).  max_steps caps the KKT solves
+        of every trajectory on both paths: the persistent solve stops a trajectory at that many
+        solves (resumable); the multi-launch loop stops once every trajectory is done or at or
+        past the cap (one launch may account up to 501 identical retries, P:151-188).
+        terminal=None: the reference's choice for the mode (par: XT = Q[0], P:73; seq:
+        hessian(final_cost), S:66)."""
         terminal = default_terminal(mode) if terminal is None else terminal
         if self.persistent:
             return self.solve_persistent(mode, terminal, bp0,
                                          max_steps if max_steps is not None else 10 ** 7)
         self.init(bp0)
-        steps = 0
-        limit = max_steps if max_steps is not None else 10 ** 9
-        while steps < limit:
+        while True:
             for _ in range(poll_every):
                 self.step(mode, terminal)
-                steps += 1
             if self.all_done():
                 break
-        return steps
+            if max_steps is not None and int(self.t["kkt_solves"].min().item()) >= max_steps:
+                break
+        return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
 
     def tiled_blocks(self):
         from .lqt import TiledBlocks

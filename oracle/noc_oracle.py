@@ -396,7 +396,8 @@ def par_newton_oc(prob, U, x0, bp, terminal="final_cost", trace=None):
             inner += 1
             if trace is not None:
                 trace.append(dict(it=it, inner=inner, reg=reg, pred=pred, gain=gain,
-                                  success=success, rp=rp))
+                                  success=success, rp=rp, cost=cost, new_cost=new_cost, hu=Hn,
+                                  bp=bp))
             if success or inner > 500:                                  # P:177-182
                 break
         X, U, Hu_norm = tX, tU, Hn                                      # P:184-188
@@ -404,11 +405,12 @@ def par_newton_oc(prob, U, x0, bp, terminal="final_cost", trace=None):
     return X, U, it, solves
 
 
-def par_interior_point_optimal_control(prob, U, x0, terminal="final_cost"):
-    """P:228-254.  Returns (U*, total outer Newton iterations, total KKT solves)."""
+def par_interior_point_optimal_control(prob, U, x0, terminal="final_cost", trace=None):
+    """P:228-254.  Returns (U*, total outer Newton iterations, total KKT solves).  trace: a
+    list that receives one dict per KKT solve (par_newton_oc)."""
     bp, total, solves = 0.1, 0, 0
     while bp > 1e-4:
-        _, U, it, s = par_newton_oc(prob, U, x0, bp, terminal)
+        _, U, it, s = par_newton_oc(prob, U, x0, bp, terminal, trace)
         bp /= 5
         total += it
         solves += s

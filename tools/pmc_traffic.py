@@ -6,9 +6,12 @@ access widths (tools/pmc_calib.hip, profiles/r02/pmc_calib: 8 B/lane reads, cont
 L = 32 two-piece tiled pattern, also count half; 8 and 16 B/lane stores count exactly) extends
 that to the whole kernel: bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  Writes
 profiles/pmc_traffic.json."""
-import csv, json, sys
+import csv, json, os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "ip-parallel-optimal-control_amd"))
+from noc._lib import source_hash  # noqa: E402  (pure Python: no library load)
 fetch_csv, write_csv, key, out = sys.argv[1:5]
-kname = sys.argv[5] if len(sys.argv) > 5 else "kkt_"
+kname = sys.argv[5] if len(sys.argv) > 5 else "kkt_scan"  # or kkt_group8
 
 def mean(path, counter):
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
@@ -23,7 +26,8 @@ except Exception:
     d = {}
 d[key] = (2 * f + w) * 1024
 d[key + "_raw"] = {"FETCH_SIZE_KB": f, "WRITE_SIZE_KB": w, "launches": [nf, nw],
-                   "kernel_filter": kname,
+                   "kernel_filter": kname, "source_hash": source_hash(kname),
+                   "fetch_csv": fetch_csv, "write_csv": write_csv,
                    "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950; calibrated for 16 and 8 B/lane reads and stores, profiles/r02/pmc_calib)"}
 json.dump(d, open(out, "w"), indent=1)
 print(key, d[key])
