@@ -451,15 +451,10 @@ struct ArgsSrc {
 // registers once, all loads issued up front, and phases 1, 3 and 4 read it from there -- one pass
 // over the blocks and one exposed memory latency instead of three dependent load chains (small
 // nx with one- or two-stage chunks, c2).
-// RELOAD (with CACHE > 0): the chunk is loaded into registers twice, every load issued up front
-// both times -- for phase 1, and again for phases 3 and 4 -- so the registers are free during the
-// cross-lane scan (the one-wave-per-SIMD instance for small batches, nx = 4: two passes over the
-// blocks and two exposed latencies instead of three passes and one latency per stage).
 // HANDOFF: phase 3 hands the chunk's first stage (A, B) to phase 4 in registers (standalone
 // scan: −1 stage of phase 4's re-reads); off inside the persistent solver, whose register budget
 // it would push into scratch (444 -> 516 B/lane).
-template <int NX, int NU, int L, bool AFF, bool TILED, class SRC, int CACHE = 0, bool HANDOFF = true,
-          bool RELOAD = false>
+template <int NX, int NU, int L, bool AFF, bool TILED, class SRC, int CACHE = 0, bool HANDOFF = true>
 NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, const SRC& src) {
   constexpr int KD = kd_width<NX, NU>();
   if (traj >= a.B) return;                     // uniform over the segment
@@ -474,7 +469,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   const int cmax = base + (rem ? 1 : 0);
   NOC_STAMP(0);
   StageData<NX, NU> cache[CACHE > 0 ? CACHE : 1];
-  if constexpr (CACHE > 0 && !RELOAD) {
+  if constexpr (CACHE > 0) {
     if (a.mode != MODE_FWD) {
       NOC_UNROLL for (int jj = 0; jj < CACHE; ++jj)
         if (jj < len) src.stage(start + jj, jj, reg, cache[jj]);
@@ -509,13 +504,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       set_zero(e.nu);
       set_zero(e.J);
     }
-    if constexpr (CACHE > 0 && RELOAD) {  // first pass: every load of the chunk issued up front
-      StageData<NX, NU> pf[CACHE];
-      NOC_UNROLL for (int jj = 0; jj < CACHE; ++jj)
-        if (jj < len) src.stage(start + jj, jj, reg, pf[jj]);
-      NOC_UNROLL for (int jj = CACHE - 1; jj >= 0; --jj)
-        if (jj < len) prepend<NX, NU, AFF>(e, pf[jj], reg);
-    } else if constexpr (CACHE > 0) {
+    if constexpr (CACHE > 0) {
       NOC_UNROLL for (int jj = CACHE - 1; jj >= 0; --jj)
         if (jj < len) prepend<NX, NU, AFF>(e, cache[jj], reg);
     } else {
@@ -659,10 +648,6 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       Phi = Pn;
     };
     if constexpr (CACHE > 0) {
-      if constexpr (RELOAD) {  // second pass, again all up front; kept for phase 4's A, B
-        NOC_UNROLL for (int jj = 0; jj < CACHE; ++jj)
-          if (jj < len) src_re.stage(start + jj, jj, reg, cache[jj]);
-      }
       NOC_UNROLL for (int jj = CACHE - 1; jj >= 0; --jj)
         if (jj < len) riccati_stage(start + jj, cache[jj]);
     } else {
@@ -879,13 +864,12 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   NOC_STAMP(6);
 }
 
-template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE = 0, bool HANDOFF = true,
-          bool RELOAD = false>
+template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE = 0, bool HANDOFF = true>
 NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
   const int cmax = a.N / L + (a.N % L ? 1 : 0);
   const ArgsSrc<NX, NU, L, AFF, TILED> src{a, traj, l, cmax, (size_t)traj * a.N};
-  kkt_scan_wave_src<NX, NU, L, AFF, TILED, ArgsSrc<NX, NU, L, AFF, TILED>, CACHE, HANDOFF, RELOAD>(
-      a, traj, l, src);
+  kkt_scan_wave_src<NX, NU, L, AFF, TILED, ArgsSrc<NX, NU, L, AFF, TILED>, CACHE, HANDOFF>(a, traj, l,
+                                                                                          src);
 }
 
 template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE>
@@ -898,21 +882,6 @@ __global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KK
 // scan element (nx = 2: 17 doubles per stage) and the lane count makes chunks short.
 template <int NX, int NU, int L>
 constexpr int kkt_cache_len() { return (NX <= 2 && L >= 32) ? 2 : 0; }
-
-// Batches that give at most one wave per SIMD (the shards of the north-star curve: 512 or 1024
-// cart-poles per GPU at 64 lanes) are latency-bound chains of one wave each: this instance has the
-// one-wave register budget (512 registers, the upper half AGPRs) and loads a lane's whole chunk of
-// up to kkt_reload_len stages with every load issued up front, once for phase 1 and once for
-// phases 3 + 4 (RELOAD), instead of one dependent load per stage in three passes.
-template <int NX, int NU, int L>
-constexpr int kkt_reload_len() { return (NX == 4 && NU == 1 && L == 64) ? 4 : 0; }
-
-template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE>
-__global__ __launch_bounds__(64, 1) void kkt_scan_kernel_w1(KKTArgs a) {
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  kkt_scan_wave<NX, NU, L, AFF, TILED, CACHE, true, true>(a, tid / L, tid % L);
-}
-
 
 
 // ---------------------------------------------------------------------------------------------
@@ -928,20 +897,8 @@ hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
   a.lds_out = lds > 0 ? 1 : 0;
   if (!a.lds_out && (!a.K || !a.d)) return hipErrorInvalidValue;  // K/d needed as workspace
   constexpr int CC = kkt_cache_len<NX, NU, L>();
-  constexpr int CR = kkt_reload_len<NX, NU, L>();
   const int cmax = a.N / L + (a.N % L ? 1 : 0);
   const bool cached = CC > 0 && cmax <= CC && !(a.ablate & 8);  // ablation bit 3: streamed chunks
-  const bool reload = CR > 0 && cmax <= CR && !(a.ablate & 8) && a.mode == MODE_FULL &&
-                      (long long)grid <= (long long)device_simd_count();
-  if constexpr (CR > 0) {
-    if (reload) {
-      if (a.tiled)
-        hipLaunchKernelGGL((kkt_scan_kernel_w1<NX, NU, L, AFF, true, CR>), dim3(grid), dim3(block), lds, stream, a);
-      else
-        hipLaunchKernelGGL((kkt_scan_kernel_w1<NX, NU, L, AFF, false, CR>), dim3(grid), dim3(block), lds, stream, a);
-      return hipGetLastError();
-    }
-  }
   if (cached) {
     if (a.tiled)
       hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, CC>), dim3(grid), dim3(block), lds, stream, a);

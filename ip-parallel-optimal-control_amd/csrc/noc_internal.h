@@ -40,21 +40,6 @@ inline size_t kkt_lds_bytes_rt(int nx, int nu, int N, int L) {
   return bytes <= 20480 ? bytes : 0;
 }
 
-// SIMDs of the current device (4 per CU), cached; 1024 (MI355X: 256 CUs) when the query fails.
-inline int device_simd_count() {
-  static int simds = 0;
-  if (simds == 0) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-      simds = 4 * cus;
-    else
-      simds = 1024;
-    (void)hipGetLastError();
-  }
-  return simds;
-}
-
 // Retry fixed point of the par inner loop (P:151-188).  A rejected trial whose rp was already at
 // the upper clip (P:173: rp * r_inc clipped back to 1e16) leaves every input of the next par_Newton
 // call unchanged -- x, u, the LQ blocks, rp -- so every remaining retry of the iteration repeats
