@@ -83,7 +83,7 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
     double c = 0.0;
     bool ok = true;
     for (int t = start; t < start + len; ++t) {
-      ok = ok && f.feasible(Us + (size_t)t * NU);
+      ok = ok && f.feasible(Xs + (size_t)t * NX, Us + (size_t)t * NU);
       c += f.stage_cost(Xs + (size_t)t * NX, Us + (size_t)t * NU, bp);
     }
     feasible = __all(ok);
@@ -154,10 +154,8 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
         double Vx[NX], Vxx[NX * NX];
         {
           const double* xN = X + (size_t)N * NX;
-          NOC_UNROLL for (int i = 0; i < NX; ++i) {
-            Vx[i] = prm.wf[i] * f.err(xN, i);
-            NOC_UNROLL for (int j = 0; j < NX; ++j) Vxx[i * NX + j] = (i == j) ? prm.wf[i] : 0.0;
-          }
+          f.final_grad(xN, Vx);
+          f.final_hess(xN, Vxx);
         }
         double pred = 0.0;
         bool feas = true;
@@ -343,6 +341,11 @@ static hipError_t ddp_family(const noc_family& p, const DdpArgs& a, hipStream_t 
 }
 
 bool ddp_supported(const noc_family& p) {
+#ifdef NOC_CUSTOM_FAMILY
+  // a registered family with its own traced cost: the DDP record keeps the parametrised cost's
+  // diagonal Hessians only (the interior-point Newton solvers take any cost)
+  if (p.kind == NOC_FAMILY_CUSTOM && gen::kCustomCost) return false;
+#endif
   return family_supported(p) && p.nx <= 4;  // one wave holds the nx x nx value Hessian
 }
 

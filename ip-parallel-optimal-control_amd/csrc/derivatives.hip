@@ -33,13 +33,16 @@ __global__ __launch_bounds__(256) void derivatives_kernel(noc_family prm, DerivA
   f.stage_grad(x, u, bp, cx, cu);
   NOC_UNROLL for (int i = 0; i < NX; ++i) a.cx[bk * NX + i] = cx[i];
   NOC_UNROLL for (int j = 0; j < NU; ++j) a.cu[bk * NU + j] = cu[j];
-  // cxx = diag(wx) (the wrapped coordinate's mod has derivative 1), cuu = diag(wu + barrier),
-  // cxu = 0: the Hessians of the quadratic-plus-log-barrier stage cost (PR:40-50, CR:36-45)
-  NOC_UNROLL for (int i = 0; i < NX; ++i)
-    NOC_UNROLL for (int j = 0; j < NX; ++j) a.cxx[(bk * NX + i) * NX + j] = (i == j) ? prm.wx[i] : 0.0;
-  NOC_UNROLL for (int i = 0; i < NU; ++i)
-    NOC_UNROLL for (int j = 0; j < NU; ++j) a.cuu[(bk * NU + i) * NU + j] = (i == j) ? f.stage_cuu(u, bp, i) : 0.0;
-  NOC_UNROLL for (int i = 0; i < NX * NU; ++i) a.cxu[bk * NX * NU + i] = 0.0;
+  // cxx, cuu, cxu: the stage cost's Hessian (ipm_family.h: stage_hess; for the quadratic-plus-
+  // log-barrier cost of PR:40-50 / CR:36-45 diag(wx), diag(wu + barrier), 0 -- the wrapped
+  // coordinate's mod has derivative 1)
+  {
+    double cxx[NX * NX], cuu[NU * NU], cxu[NX * NU];
+    f.stage_hess(x, u, bp, cxx, cuu, cxu);
+    NOC_UNROLL for (int i = 0; i < NX * NX; ++i) a.cxx[bk * NX * NX + i] = cxx[i];
+    NOC_UNROLL for (int i = 0; i < NU * NU; ++i) a.cuu[bk * NU * NU + i] = cuu[i];
+    NOC_UNROLL for (int i = 0; i < NX * NU; ++i) a.cxu[bk * NX * NU + i] = cxu[i];
+  }
   double fx[NX * NX], fu[NX * NU];
   f.jac(x, u, fx, fu);
   NOC_UNROLL for (int i = 0; i < NX * NX; ++i) a.fx[bk * NX * NX + i] = fx[i];
@@ -68,10 +71,14 @@ __global__ __launch_bounds__(256) void final_derivs_kernel(noc_family prm, int B
   Fam<KIND, NX, NU> f(prm);
   double x[NX];
   NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = xN[(size_t)b * NX + i];
-  NOC_UNROLL for (int i = 0; i < NX; ++i) grad[(size_t)b * NX + i] = prm.wf[i] * f.err(x, i);
-  if (hess)
-    NOC_UNROLL for (int i = 0; i < NX; ++i)
-      NOC_UNROLL for (int j = 0; j < NX; ++j) hess[((size_t)b * NX + i) * NX + j] = (i == j) ? prm.wf[i] : 0.0;
+  double g[NX];
+  f.final_grad(x, g);
+  NOC_UNROLL for (int i = 0; i < NX; ++i) grad[(size_t)b * NX + i] = g[i];
+  if (hess) {
+    double H[NX * NX];
+    f.final_hess(x, H);
+    NOC_UNROLL for (int i = 0; i < NX * NX; ++i) hess[(size_t)b * NX * NX + i] = H[i];
+  }
 }
 
 template <int KIND, int NX, int NU>

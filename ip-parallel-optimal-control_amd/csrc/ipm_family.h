@@ -40,8 +40,13 @@ struct Fam {
   // the built-ins, noc/utils.py:50-54) or the discrete map x+ = F(x, u) itself (kDiscrete).
 #ifdef NOC_CUSTOM_FAMILY
   static constexpr bool kDiscrete = (KIND == NOC_FAMILY_CUSTOM) && gen::kCustomDiscrete;
+  // the family's own stage cost / final cost / constraints, traced from the user's callables
+  // (noc.families.register_family(stage_cost=..., final_cost=..., constraints=...)), instead of
+  // the parametrised quadratic tracking cost with a box log barrier on u
+  static constexpr bool kGenCost = (KIND == NOC_FAMILY_CUSTOM) && gen::kCustomCost;
 #else
   static constexpr bool kDiscrete = false;
+  static constexpr bool kGenCost = false;
 #endif
   // generated right-hand side / Jacobian J = d rhs / d[x; u] / lambda-contracted Hessian
   NOC_DEV static void rhs(const double* x, const double* u, double* f) {
@@ -127,6 +132,9 @@ struct Fam {
   NOC_DEV bool barrier() const { return p.u_bound > 0.0; }
   // stage cost (PR:40-50 / CR:36-45 / LD:138-141)
   NOC_DEV double stage_cost(const double* x, const double* u, double bp) const {
+#ifdef NOC_CUSTOM_FAMILY
+    if constexpr (kGenCost) return gen::custom_stage_cost(x, u, bp);
+#endif
     double c = 0.0;
     NOC_UNROLL for (int i = 0; i < NX; ++i) { const double e = err(x, i); c += p.wx[i] * e * e; }
     c *= 0.5;
@@ -142,6 +150,12 @@ struct Fam {
   }
   NOC_DEV void stage_grad(const double* x, const double* u, double bp, double* cx,
                           double* cu) const {
+#ifdef NOC_CUSTOM_FAMILY
+    if constexpr (kGenCost) {
+      gen::custom_stage_grad(x, u, bp, cx, cu);
+      return;
+    }
+#endif
     NOC_UNROLL for (int i = 0; i < NX; ++i) cx[i] = p.wx[i] * err(x, i);
     NOC_UNROLL for (int j = 0; j < NU; ++j) {
       double g = p.wu[j] * u[j];
@@ -157,16 +171,58 @@ struct Fam {
     }
     return h;
   }
-  NOC_DEV bool feasible(const double* u) const {  // all(constraints <= 0) (P:45-47)
+  // hessian of the stage cost (P:19-21: cxx, cuu, cxu), full row-major matrices
+  NOC_DEV void stage_hess(const double* x, const double* u, double bp, double* Q, double* R,
+                          double* M) const {
+#ifdef NOC_CUSTOM_FAMILY
+    if constexpr (kGenCost) {
+      gen::custom_stage_hess(x, u, bp, Q, R, M);
+      return;
+    }
+#endif
+    (void)x;
+    NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) Q[i * NX + j] = (i == j) ? p.wx[i] : 0.0;
+    NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int j = 0; j < NU; ++j) R[i * NU + j] = (i == j) ? stage_cuu(u, bp, i) : 0.0;
+    NOC_UNROLL for (int i = 0; i < NX * NU; ++i) M[i] = 0.0;
+  }
+  // all(constraints(x, u) <= 0) (P:45-47)
+  NOC_DEV bool feasible(const double* x, const double* u) const {
+#ifdef NOC_CUSTOM_FAMILY
+    if constexpr (kGenCost) return gen::custom_feasible(x, u);
+#endif
+    (void)x;
     if (!barrier()) return true;
     bool ok = true;
     NOC_UNROLL for (int j = 0; j < NU; ++j) ok = ok && (u[j] - p.u_bound <= 0.0) && (-u[j] - p.u_bound <= 0.0);
     return ok;
   }
   NOC_DEV double final_cost(const double* x) const {
+#ifdef NOC_CUSTOM_FAMILY
+    if constexpr (kGenCost) return gen::custom_final_cost(x);
+#endif
     double c = 0.0;
     NOC_UNROLL for (int i = 0; i < NX; ++i) { const double e = err(x, i); c += p.wf[i] * e * e; }
     return 0.5 * c;
+  }
+  // grad(final_cost) (C:35: the terminal costate) and hessian(final_cost) (S:66)
+  NOC_DEV void final_grad(const double* x, double* g) const {
+#ifdef NOC_CUSTOM_FAMILY
+    if constexpr (kGenCost) {
+      gen::custom_final_grad(x, g);
+      return;
+    }
+#endif
+    NOC_UNROLL for (int i = 0; i < NX; ++i) g[i] = p.wf[i] * err(x, i);
+  }
+  NOC_DEV void final_hess(const double* x, double* H) const {
+#ifdef NOC_CUSTOM_FAMILY
+    if constexpr (kGenCost) {
+      gen::custom_final_hess(x, H);
+      return;
+    }
+#endif
+    (void)x;
+    NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) H[i * NX + j] = (i == j) ? p.wf[i] : 0.0;
   }
 };
 

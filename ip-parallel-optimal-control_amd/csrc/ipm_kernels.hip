@@ -122,7 +122,7 @@ __global__ __launch_bounds__(64) void costate_scan_kernel(noc_family prm, noc_ip
   const bool last = (l == L - 1);
   const double* xN = w.x + ((size_t)b * (N + 1) + N) * NX;
   double lamN[NX];
-  NOC_UNROLL for (int i = 0; i < NX; ++i) lamN[i] = prm.wf[i] * f.err(xN, i);
+  f.final_grad(xN, lamN);  // grad(final_cost) (C:35)
   // phases 1-2 (L > 1): chunk maps and their scan; L = 1 (grouped layout, one lane per
   // trajectory) sweeps the whole horizon from lambda_N directly
   Mat<NX, NX> G;
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(64) void costate_scan_kernel(noc_family prm, noc_ip
   }
   if (l != 0) return;
   double P[NX * NX];
-  NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) P[i * NX + j] = (i == j) ? prm.wf[i] : 0.0;
+  f.final_hess(xN, P);  // hessian(final_cost) (S:66)
   gstore<NX * NX>(w.P + (size_t)b * NX * NX, P);
   w.cost[b] = cost + f.final_cost(xN);   // total_cost(x, u, bp) (P:142)
   w.hu[b] = hu;                          // max |Hu| (P:158)
@@ -265,9 +265,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(noc_family prm, noc_ipm_w
   gload<NX>(w.lam + ((size_t)b * (N + 1) + k + 1) * NX, lam);
   // Q = cxx + l.fxx ; R = cuu + l.fuu ; M = cxu + l.fxu  (P:35-37), l = lambda_{k+1}
   double Q[NX * NX], R[NU * NU], M[NX * NU];
-  NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int jj = 0; jj < NX; ++jj) Q[i * NX + jj] = (i == jj) ? prm.wx[i] : 0.0;
-  NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int jj = 0; jj < NU; ++jj) R[i * NU + jj] = (i == jj) ? f.stage_cuu(u, bp, i) : 0.0;
-  NOC_UNROLL for (int i = 0; i < NX * NU; ++i) M[i] = 0.0;
+  f.stage_hess(x, u, bp, Q, R, M);
   f.add_hess_l(x, u, lam, Q, R, M);
   Sym<NX> Qs;
   Sym<NU> Rs;
@@ -314,7 +312,7 @@ __global__ __launch_bounds__(256) void trial_kernel(noc_family prm, noc_ipm_ws w
     double xt[NX], ut[NU];
     NOC_UNROLL for (int i = 0; i < NX; ++i) xt[i] = X[(size_t)k * NX + i] + DX[(size_t)k * NX + i];
     NOC_UNROLL for (int j = 0; j < NU; ++j) ut[j] = U[(size_t)k * NU + j] + DU[(size_t)k * NU + j];
-    ok &= f.feasible(ut) ? 1 : 0;
+    ok &= f.feasible(xt, ut) ? 1 : 0;
     csum += f.stage_cost(xt, ut, bp);
   }
   if (lane == 63) {

@@ -197,7 +197,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         // costates as a reverse affine scan (C:34-54) fused with the LQ blocks (P:31-42)
         const double* xN = X + (size_t)N * NX;
         double lamN[NX];
-        NOC_UNROLL for (int i = 0; i < NX; ++i) lamN[i] = prm.wf[i] * f.err(xN, i);
+        f.final_grad(xN, lamN);  // grad(final_cost) (C:35)
         Mat<NX, NX> G;
         Vec<NX> g;
         set_identity(G);
@@ -278,9 +278,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         };
         auto cost_compute = [&](const StageIn& in, bool valid, StageOut& o) {
           double Q[NX * NX], R[NU * NU];
-          NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int jj = 0; jj < NX; ++jj) Q[i * NX + jj] = (i == jj) ? prm.wx[i] : 0.0;
-          NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int jj = 0; jj < NU; ++jj) R[i * NU + jj] = (i == jj) ? f.stage_cuu(in.u, bp, i) : 0.0;
-          NOC_UNROLL for (int i = 0; i < NX * NU; ++i) o.M[i] = 0.0;
+          f.stage_hess(in.x, in.u, bp, Q, R, o.M);
           f.add_hess_l(in.x, in.u, lam, Q, R, o.M);
           NOC_UNROLL for (int i = 0; i < NX; ++i)
             NOC_UNROLL for (int jj = i; jj < NX; ++jj) o.Qs(i, jj) = (i == jj) ? Q[i * NX + i] : 0.5 * (Q[i * NX + jj] + Q[jj * NX + i]);
@@ -345,7 +343,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         }
         if (terminal == NOC_TERMINAL_FINAL_COST && last) {  // hessian(final_cost) (S:66)
           double P[NX * NX];
-          NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int jj = 0; jj < NX; ++jj) P[i * NX + jj] = (i == jj) ? prm.wf[i] : 0.0;
+          f.final_hess(xN, P);
           gstore<NX * NX>(w.P + (size_t)b * NX * NX, P);
         }
         // total_cost(x, u, bp) (P:142); x_N is the last lane's own (trial) store
@@ -394,7 +392,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
           trial_load(clampk(start + j + 1), xt1, ut1);
           const double c0 = f.stage_cost(xt0, ut0, bp);
           const double c1 = f.stage_cost(xt1, ut1, bp);
-          const bool f0 = f.feasible(ut0), f1 = f.feasible(ut1);
+          const bool f0 = f.feasible(xt0, ut0), f1 = f.feasible(xt1, ut1);
           if (j < len) { ok &= f0 ? 1 : 0; tsum += c0; }
           if (j + 1 < len) { ok &= f1 ? 1 : 0; tsum += c1; }
         }
@@ -402,7 +400,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         for (int j = 0; j < len; ++j) {
           double xt[NX], ut[NU];
           trial_load(start + j, xt, ut);
-          ok &= f.feasible(ut) ? 1 : 0;
+          ok &= f.feasible(xt, ut) ? 1 : 0;
           tsum += f.stage_cost(xt, ut, bp);
         }
       }

@@ -283,7 +283,7 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
         // the waves joined through LDS, then the sweep fused with the LQ blocks (P:31-42)
         const double* xN = sx + (size_t)N * NX;
         double lamN[NX];
-        NOC_UNROLL for (int i = 0; i < NX; ++i) lamN[i] = prm.wf[i] * f.err(xN, i);
+        f.final_grad(xN, lamN);  // grad(final_cost) (C:35)
         Mat<NX, NX> G;
         Vec<NX> g;
         set_identity(G);
@@ -379,9 +379,7 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
           fget<NU>(scu, N, s, cu);
           // Q = cxx + l.fxx, R = cuu + l.fuu, M = cxu + l.fxu at l = lambda_{s+1} (P:35-37)
           double Qf[NX * NX], Rf[NU * NU], M[NX * NU], rr[NU];
-          NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) Qf[i * NX + j] = (i == j) ? prm.wx[i] : 0.0;
-          NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int j = 0; j < NU; ++j) Rf[i * NU + j] = (i == j) ? f.stage_cuu(u, bp, i) : 0.0;
-          NOC_UNROLL for (int i = 0; i < NX * NU; ++i) M[i] = 0.0;
+          f.stage_hess(x, u, bp, Qf, Rf, M);
           f.add_hess_l(x, u, lam, Qf, Rf, M);
           Sym<NX> Qs;
           Sym<NU> Rs;
@@ -411,8 +409,7 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
           NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = ln[i];
           red[0] += slc[s];
         }
-        if (terminal == NOC_TERMINAL_FINAL_COST && last)  // hessian(final_cost) (S:66)
-          NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) sP[i * NX + j] = (i == j) ? prm.wf[i] : 0.0;
+        if (terminal == NOC_TERMINAL_FINAL_COST && last) f.final_hess(xN, sP);  // S:66
         const bool is_max[4] = {false, true, false, false};
         wg_reduce(red, 3, is_max);
         cost = red[0] + f.final_cost(xN);  // total_cost(x, u, bp) (P:142)
@@ -696,7 +693,7 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
         double xt[NX], ut[NU];
         NOC_UNROLL for (int i = 0; i < NX; ++i) xt[i] = sx[(size_t)s * NX + i] + dxs(i, s);
         NOC_UNROLL for (int j = 0; j < NU; ++j) ut[j] = su[(size_t)j * N + s] + dus(j, s);
-        ok &= f.feasible(ut) ? 1 : 0;
+        ok &= f.feasible(xt, ut) ? 1 : 0;
         tr[0] += f.stage_cost(xt, ut, bp);
       }
       if (last) {

@@ -39,6 +39,36 @@ class _DevicePrinter(C99CodePrinter):
         return super()._print_Pow(expr)
 
 
+    def _print_PyMod(self, expr):
+        a, b = expr.args
+        return f"noc_pymod({self._print(a)}, {self._print(b)})"
+
+
+class PyMod(sp.Function):
+    """a mod b with the sign of b -- Python's / jnp's `%` (the reference's wrap_angle, U:8-10) --
+    with the derivative jax.grad gives it: d/da = 1 (sympy leaves Mod's derivative unevaluated).
+    Printed as noc_pymod() (defined in the generated header)."""
+    nargs = 2
+
+    def fdiff(self, argindex=1):
+        a, b = self.args
+        return sp.Integer(1) if argindex == 1 else -sp.floor(a / b)
+
+
+def _pymod(e):
+    """Mod(a, b) -> PyMod(a, b) (differentiable, printed with Python remainder semantics)."""
+    return e.replace(lambda t: isinstance(t, sp.Mod), lambda t: PyMod(*t.args))
+
+
+# device helper of the generated cost code: Python / jnp remainder (sign of the divisor); the
+# general fmod routine only outside |a| < |b|, where fmod(a, b) == a exactly
+PYMOD_DEVICE = """NOC_DEV double noc_pymod(double a, double b) {
+  double r = a;
+  if (!(fabs(a) < fabs(b))) r = fmod(a, b);
+  return (r != 0.0 && ((r < 0.0) != (b < 0.0))) ? r + b : r;
+}"""
+
+
 def _ccode(e) -> str:
     return _DevicePrinter().doprint(e)
 
@@ -135,3 +165,80 @@ def trace(fn, nx: int, nu: int):
     if free:
         raise ValueError(f"the dynamics depend on symbols other than the state / control: {free}")
     return X, U, out
+
+
+def _block(lines, sig, exprs, targets, X, U, extra=(), ret=None):
+    """One straight-line device function: CSE over `exprs`, shared sincos of the states, the
+    results assigned to `targets` (or returned: ret = "value" / "all_nonpositive")."""
+    exprs, pre = _trig_subst([_pymod(sp.sympify(e)) for e in exprs], X)
+    reps, red = sp.cse(exprs, symbols=sp.numbered_symbols("t"))
+    lines.append(sig + " {")
+    for i in range(len(X)):
+        lines.append(f"  [[maybe_unused]] const double x{i} = x[{i}];")
+    for i in range(len(U)):
+        lines.append(f"  [[maybe_unused]] const double u{i} = u[{i}];")
+    lines.extend(pre)
+    lines.extend(f"  const double {_ccode(s_)} = {_ccode(e)};" for s_, e in reps)
+    if ret == "value":
+        lines.append(f"  return {_ccode(red[0])};")
+    elif ret == "all_nonpositive":
+        conds = " && ".join(f"({_ccode(e)} <= 0.0)" for e in red) or "true"
+        lines.append(f"  return {conds};")
+    else:
+        lines.extend(f"  {t} = {_ccode(e)};" for t, e in zip(targets, red))
+    lines.append("}")
+
+
+def emit_costs(name, X, U, bp, stage, final, cons):
+    """Device functions of a user cost (the reference OCP's stage_cost / final_cost / constraints,
+    T:5-10, differentiated like P:13-28 does with jax.grad / hessian):
+    {name}_stage_cost(x, u, bp), _stage_grad(x, u, bp, cx, cu), _stage_hess(x, u, bp, Q, R, M)
+    (Q = d2/dx2, R = d2/du2, M = d2/dxdu, row-major), {name}_final_cost(x), _final_grad(x, g),
+    _final_hess(x, H), and {name}_feasible(x, u) = all(constraints(x, u) <= 0) (P:45-47)."""
+    nx, nu = len(X), len(U)
+    stage, final = _pymod(sp.sympify(stage)), _pymod(sp.sympify(final))
+    cx = [sp.diff(stage, xi) for xi in X]
+    cu = [sp.diff(stage, ui) for ui in U]
+    Q = [sp.diff(stage, X[i], X[j]) for i in range(nx) for j in range(nx)]
+    R = [sp.diff(stage, U[i], U[j]) for i in range(nu) for j in range(nu)]
+    M = [sp.diff(stage, X[i], U[j]) for i in range(nx) for j in range(nu)]
+    g = [sp.diff(final, xi) for xi in X]
+    H = [sp.diff(final, X[i], X[j]) for i in range(nx) for j in range(nx)]
+    lines = []
+    a_xub = "const double* x, const double* u, double bp"
+    _block(lines, f"NOC_DEV double {name}_stage_cost({a_xub})", [stage], [], X, U, ret="value")
+    _block(lines, f"NOC_DEV void {name}_stage_grad({a_xub}, double* cx, double* cu)",
+           cx + cu, [f"cx[{i}]" for i in range(nx)] + [f"cu[{j}]" for j in range(nu)], X, U)
+    _block(lines, f"NOC_DEV void {name}_stage_hess({a_xub}, double* Q, double* R, double* M)",
+           Q + R + M, [f"Q[{k}]" for k in range(nx * nx)] + [f"R[{k}]" for k in range(nu * nu)] +
+           [f"M[{k}]" for k in range(nx * nu)], X, U)
+    _block(lines, f"NOC_DEV double {name}_final_cost(const double* x)", [final], [], X, [],
+           ret="value")
+    _block(lines, f"NOC_DEV void {name}_final_grad(const double* x, double* g)", g,
+           [f"g[{i}]" for i in range(nx)], X, [])
+    _block(lines, f"NOC_DEV void {name}_final_hess(const double* x, double* H)", H,
+           [f"H[{k}]" for k in range(nx * nx)], X, [])
+    _block(lines, f"NOC_DEV bool {name}_feasible(const double* x, const double* u)",
+           list(cons), [], X, U, ret="all_nonpositive")
+    return "\n".join(lines)
+
+
+def trace_costs(stage_cost, final_cost, constraints, nx: int, nu: int):
+    """Call the user's stage_cost(x, u, bp), final_cost(x) and constraints(x, u) (numpy, like the
+    reference examples' CR:18-51) on symbolic arrays; returns (X, U, bp, stage, final, cons)."""
+    X = list(sp.symbols(f"x0:{nx}", real=True))
+    U = list(sp.symbols(f"u0:{nu}", real=True))
+    bp = sp.Symbol("bp", real=True)
+    xa, ua = np.array(X, dtype=object), np.array(U, dtype=object)
+    with _sympy_ufuncs():
+        stage = sp.sympify(np.asarray(stage_cost(xa, ua, bp), dtype=object).reshape(-1)[0])
+        final = sp.sympify(np.asarray(final_cost(xa), dtype=object).reshape(-1)[0])
+        cons = [] if constraints is None else \
+            [sp.sympify(e) for e in np.asarray(constraints(xa, ua), dtype=object).reshape(-1)]
+    for what, es, allowed in (("stage_cost", [stage], set(X) | set(U) | {bp}),
+                              ("final_cost", [final], set(X)),
+                              ("constraints", cons, set(X) | set(U))):
+        free = set().union(set(), *(e.free_symbols for e in es)) - allowed
+        if free:
+            raise ValueError(f"{what} depends on symbols other than its arguments: {free}")
+    return X, U, bp, stage, final, cons

@@ -53,3 +53,60 @@ def test_committed_families_gen_is_the_generator_output():
         committed = fh.read()
     assert committed == gen_family_derivs.render()
     assert "pow(" not in committed
+
+
+def test_traced_costs_match_torch_autodiff():
+    """register_family's cost tracing (noc/_codegen.trace_costs): the symbolic stage / final
+    cost, gradients and Hessians of the track-limited cart-pole's numpy callables -- wrapped
+    angle (`%`, derivative 1 like jax.grad), log barrier with a state constraint, quartic term --
+    against torch.func on the independent torch restatement, at random feasible points (CPU)."""
+    import numpy as np
+    import sympy as sp
+    import torch
+    import custom_families as CF
+    from noc import _codegen
+    X, U, bp, stage, final, cons = _codegen.trace_costs(
+        CF.track_limit_stage_cost, CF.track_limit_final_cost, CF.track_limit_constraints, 4, 1)
+    stage, final = _codegen._pymod(stage), _codegen._pymod(final)
+    mods = [{"PyMod": lambda a, b: np.mod(a, b)}, "numpy"]
+    z = X + U
+    f_s = sp.lambdify(z + [bp], stage, mods)
+    g_s = sp.lambdify(z + [bp], [sp.diff(stage, v) for v in z], mods)
+    h_s = sp.lambdify(z + [bp], [[sp.diff(stage, a, b) for b in z] for a in z], mods)
+    g_f = sp.lambdify(X, [sp.diff(final, v) for v in X], mods)
+    h_f = sp.lambdify(X, [[sp.diff(final, a, b) for b in X] for a in X], mods)
+    t = CF.cartpole_track_limit_torch(0.02)
+    rng = np.random.default_rng(0)
+    for _ in range(5):
+        x = np.array([0.8 * CF.X_LIMIT * rng.uniform(-1, 1), rng.uniform(-7, 7), rng.normal(),
+                      rng.normal()])
+        u = np.array([rng.uniform(-40, 40)])
+        bpv = 0.1 * rng.uniform()
+        xt, ut = torch.tensor(x), torch.tensor(u)
+        sc = lambda zz: t.stage_cost(zz[:4], zz[4:], bpv)
+        zt = torch.cat((xt, ut))
+        assert abs(f_s(*x, *u, bpv) - float(sc(zt))) <= 1e-12 * abs(float(sc(zt)))
+        assert np.allclose(g_s(*x, *u, bpv), torch.func.grad(sc)(zt).numpy(), rtol=1e-12, atol=1e-12)
+        assert np.allclose(np.array(h_s(*x, *u, bpv), dtype=float),
+                           torch.func.hessian(sc)(zt).numpy(), rtol=1e-12, atol=1e-12)
+        assert np.allclose(g_f(*x), torch.func.grad(t.final_cost)(xt).numpy(), rtol=1e-12, atol=1e-12)
+        assert np.allclose(np.array(h_f(*x), dtype=float), torch.func.hessian(t.final_cost)(xt).numpy(),
+                           rtol=1e-12, atol=1e-12)
+        feas = all(float(c.subs({**dict(zip(X, x)), U[0]: u[0]})) <= 0 for c in cons)
+        assert feas == bool(torch.all(t.constraints(xt, ut) <= 0))
+
+
+def test_traced_cost_header_compiles_into_a_family_header():
+    """The generated custom_family_gen.h carries the cost functions and kCustomCost; a dynamics-
+    only family gets stubs and kCustomCost = false."""
+    import custom_families as CF
+    from noc import families
+    h = families.generate_header("tl", CF.cartpole_ode, 4, 1, False,
+                                 (CF.track_limit_stage_cost, CF.track_limit_final_cost,
+                                  CF.track_limit_constraints))
+    for name in ("custom_stage_cost", "custom_stage_grad", "custom_stage_hess", "custom_final_cost",
+                 "custom_final_grad", "custom_final_hess", "custom_feasible", "noc_pymod"):
+        assert f"{name}(" in h
+    assert "constexpr bool kCustomCost = true;" in h
+    h0 = families.generate_header("ap", CF.actuated_pendulum_ode, 3, 1, False)
+    assert "constexpr bool kCustomCost = false;" in h0 and "custom_feasible(" in h0

@@ -111,3 +111,106 @@ def test_kkt_solve_on_the_custom_shape(lanes):
     torch.cuda.synchronize()
     for k in ("dx", "du", "K", "d", "S", "v", "pred"):
         assert _rel(getattr(out, k).cpu().numpy(), ref[k]) < 1e-10, k
+
+
+# ------------------------------------------------------------------------------------------------
+# a family with the reference OCP's own kind of callables: traced stage / final costs (a quartic
+# term) and a STATE constraint (cart within +-X_LIMIT) inside the log barrier
+# ------------------------------------------------------------------------------------------------
+def _tl_inputs(N, B, seed):
+    from noc import problems
+    return problems.initial_conditions("cartpole", N, B, seed=seed)
+
+
+def test_traced_cost_linearisation_matches_autodiff():
+    """compute_derivatives (P:13-28) of the traced costs: every derivative array of the
+    Derivatives type (cx, cu, cxx, cuu, cxu) and the LQ blocks against torch.func on the torch
+    restatement, at 1e-10; the final-cost gradient / Hessian; the total cost."""
+    from noc import _lib
+    from noc.ipm import BatchedIPM
+    from noc.par_interior_point_newton import compute_derivatives
+    from oracle import noc_oracle as O
+    import custom_families as CF
+    N, B = 50, 3
+    ocp = CF.cartpole_track_limit(1.0 / N)
+    x0, u0 = _tl_inputs(N, B, 3)
+    eng = BatchedIPM(ocp.family, N, B, lanes=64)
+    eng.load(u0, x0)
+    eng.init(bp0=0.1)
+    eng.prepare(mode=_lib.MODE_PAR, terminal=_lib.TERMINAL_FINAL_COST)
+    nat = eng.natural_blocks()
+    torch.cuda.synchronize()
+    prob = O.NumpyProblem(CF.cartpole_track_limit_torch(1.0 / N))
+    X = eng.t["x"].cpu().numpy()
+    d = compute_derivatives(ocp, X, u0, 0.1)
+    for b in range(B):
+        assert _rel(X[b], O.rollout(prob.dynamics, u0[b], x0[b])) < 1e-12
+        ref = prob.derivatives(X[b], u0[b], 0.1)
+        for k, got in enumerate(d):
+            assert _rel(got[b].cpu().numpy(), ref[k]) < 1e-10, k
+        L = O.linearize(prob, X[b], u0[b], 0.1)
+        for k in ("A", "B", "Q", "R", "M", "r", "P"):
+            assert _rel(nat[k][b].cpu().numpy(), L[k]) < 1e-10, k
+        cost = prob.total_cost(X[b], u0[b], 0.1)
+        assert abs(eng.t["cost"][b].item() - cost) <= 1e-12 * abs(cost)
+        assert abs(ocp.total_cost(X[b], u0[b], 0.1) - cost) <= 1e-12 * abs(cost)
+
+
+def test_traced_cost_state_constraint_solve_matches_oracle():
+    """The whole par interior-point solve (P:228-254, persistent kernel) of the track-limited
+    cart-pole: identical outer iterations and KKT solves per trajectory as the oracle loop on the
+    torch restatement, controls within 1e-6; the state constraint holds on the solver's states
+    and is active (the cart reaches the limit: the swing-up wants more track)."""
+    from noc.par_interior_point_newton import par_interior_point_optimal_control
+    from oracle import noc_oracle as O
+    import custom_families as CF
+    N, B = 50, 2
+    ocp = CF.cartpole_track_limit(1.0 / N)
+    x0, u0 = _tl_inputs(N, B, 3)
+    U, its, info = par_interior_point_optimal_control(ocp, u0, x0, return_info=True)
+    prob = O.NumpyProblem(CF.cartpole_track_limit_torch(1.0 / N))
+    for b in range(B):
+        Ur, itr, sr = O.par_interior_point_optimal_control(prob, u0[b], x0[b], terminal="stage0")
+        assert its[b] == itr and info["kkt_solves"][b] == sr, (b, its[b], itr, info["kkt_solves"][b], sr)
+        assert np.max(np.abs(U[b] - Ur)) < 1e-6
+
+
+def test_traced_cost_state_constraint_active_and_respected():
+    """On the solver's own states (x + dx of the kept steps, P:184) the trial feasibility test
+    (P:45-47, with the state constraint) held at every accepted step: |cart| <= X_LIMIT, and the
+    optimum presses against it.  The multi-launch loop gives the same iterates."""
+    from noc import _lib
+    from noc.ipm import BatchedIPM
+    import custom_families as CF
+    N, B = 50, 4
+    ocp = CF.cartpole_track_limit(1.0 / N)
+    x0, u0 = _tl_inputs(N, B, 3)
+    res = []
+    for persistent in (True, False):
+        eng = BatchedIPM(ocp.family, N, B, lanes=64, persistent=persistent)
+        eng.load(u0, x0)
+        eng.solve()
+        torch.cuda.synchronize()
+        res.append([t.cpu().numpy() for t in eng.result()] + [eng.t["x"].cpu().numpy()])
+    (Up, itp, sp, Xp), (Um, itm, sm, Xm) = res
+    assert np.array_equal(itp, itm) and np.array_equal(sp, sm)
+    assert np.max(np.abs(Up - Um)) <= 1e-12 * max(1.0, float(np.max(np.abs(Um))))
+    xc = np.abs(Xp[:, :-1, 0])
+    assert np.all(xc <= CF.X_LIMIT) and np.all(xc.max(axis=1) > 0.9 * CF.X_LIMIT)
+
+
+def test_traced_cost_family_rejects_ddp_and_mixed_costs():
+    from noc import _lib
+    from noc import families
+    import custom_families as CF
+    ocp = CF.cartpole_track_limit(1.0 / 50)
+    lib = _lib.load_for(ocp.family)
+    import ctypes
+    assert lib.noc_ddp_supported(ctypes.byref(ocp.family.to_c())) == 0
+    with pytest.raises(_lib.NocError):
+        families.register_family("bad", CF.cartpole_ode, 4, 1, dt=0.02,
+                                 stage_cost=CF.track_limit_stage_cost, build=False)
+    with pytest.raises(_lib.NocError):
+        families.register_family("bad", CF.cartpole_ode, 4, 1, dt=0.02, wx=[1.0] * 4,
+                                 stage_cost=CF.track_limit_stage_cost,
+                                 final_cost=CF.track_limit_final_cost, build=False)
