@@ -24,9 +24,10 @@
  *
  * Supported (nx, nu): (2,1) pendulum, (4,1) cart-pole, (8,4) stacked double integrators.
  * `lanes` = lanes of a wave64 per trajectory (64, 32, 16, 8: parallel-in-time scan over the
- * horizon, chunked over the lanes); 1 = horizon-sequential Riccati with the trajectory's algebra
- * spread over an nx-lane group (work-efficient; for batches that fill the GPU by themselves,
- * natural layout, gains through HBM); 0 = library default.
+ * horizon, chunked over the lanes; 128: two waves per trajectory joined through LDS, nx <= 4, for
+ * batches too small to give every SIMD a wave); 1 = horizon-sequential Riccati with the
+ * trajectory's algebra spread over an nx-lane group (work-efficient; for batches that fill the
+ * GPU by themselves, natural layout, gains through HBM); 0 = library default.
  */
 #ifndef NOC_HIP_H
 #define NOC_HIP_H
@@ -83,7 +84,7 @@ long long noc_tiled_doubles(int N, int B, int lanes, int E);
 int noc_relayout(int direction, int E, int sym_n, int N, int B, int lanes, const double* src,
                  double* dst, void* stream);
 /* noc_kkt_solve with A, Bm, Q(packed), R(packed), M, r, q, c, K, d in the tiled layout of
- * `lanes` (required, 8/16/32/64); P, p, x0, reg, dx, du, S, v natural. */
+ * `lanes` (required, 8/16/32/64/128); P, p, x0, reg, dx, du, S, v natural. */
 int noc_kkt_solve_tiled(int nx, int nu, int N, int B, int lanes,
                         const double* A, const double* Bm, const double* Q, const double* R,
                         const double* M, const double* r, const double* q, const double* c,

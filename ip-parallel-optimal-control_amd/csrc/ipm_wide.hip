@@ -83,56 +83,6 @@ NOC_DEV void fput(double* base, int N, int s, const double* v) {
   NOC_UNROLL for (int e = 0; e < E; ++e) base[(size_t)e * N + s] = v[e];
 }
 
-// e1 <- e1 (x) (value-only e2 = (J2, nu2)): the true value function at e1's start given the value
-// at its end (the VALUE_ONLY branch of combine_sklansky with the partner given explicitly)
-template <int NX>
-NOC_DEV void apply_value(Elem<NX>& e1, const Sym<NX>& J2, const Vec<NX>& nu2) {
-  double X[NX][NX], Y[NX][NX];
-  auto build = [&]() {
-    NOC_UNROLL for (int i = 0; i < NX; ++i)
-      NOC_UNROLL for (int j = 0; j < NX; ++j) {
-        double s = (i == j) ? 1.0 : 0.0;
-        NOC_UNROLL for (int k = 0; k < NX; ++k) s += e1.C(i, k) * J2(k, j);
-        X[i][j] = s;
-        Y[i][j] = e1.A(i, j);
-      }
-  };
-  build();
-  Mat<NX, NX> J2A1;
-  Vec<NX> w;
-  NOC_UNROLL for (int i = 0; i < NX; ++i) {
-    double sw = nu2[i];
-    NOC_UNROLL for (int k = 0; k < NX; ++k) sw += J2(i, k) * e1.b[k];
-    w[i] = sw;
-    NOC_UNROLL for (int j = 0; j < NX; ++j) {
-      double s = 0.0;
-      NOC_UNROLL for (int k = 0; k < NX; ++k) s += J2(i, k) * e1.A(k, j);
-      J2A1(i, j) = s;
-    }
-  }
-  // nx = 2: closed form (det(I + C1 J2) >= 1), as combine_sklansky; else the threshold-checked
-  // elimination with a per-lane fallback (no shuffles here, so no uniformity is needed)
-  if constexpr (NX == 2) {
-    solve2_closed<NX>(X, Y);
-  } else if (!lu_np_solve<NX, NX>(X, Y)) {
-    build();
-    lu_pp_solve<NX, NX>(X, Y);
-  }
-  NOC_UNROLL for (int i = 0; i < NX; ++i) {
-    NOC_UNROLL for (int j = i; j < NX; ++j) {
-      double s = e1.J(i, j);
-      NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * J2A1(k, j);
-      e1.J(i, j) = s;
-    }
-    double s = e1.nu[i];
-    NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * w[k];
-    e1.nu[i] = s;
-  }
-  set_zero(e1.A);
-  set_zero(e1.b);
-  set_zero(e1.C);
-}
-
 template <int NX>
 NOC_DEV void elem_put(double* p, const Elem<NX>& e) {
   int o = 0;
@@ -166,6 +116,11 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
   constexpr int ESZ = NX * NX + 2 * NX + 2 * Sym<NX>::SZ;  // scan element in doubles
   static_assert(ESZ <= 64 && NX * NX + NX <= 64, "aggregate slot");
   extern __shared__ __attribute__((aligned(16))) double noc_smem[];
+  // one wave per SIMD: the W waves of the workgroup on W different SIMDs.  With fewer registers
+  // (pendulum: 189 VGPRs, two waves could share a SIMD) the dispatcher may stack the workgroup's
+  // waves on fewer SIMDs than the CU has, and their VALU-bound scans then take turns; claiming the
+  // whole register file rules that out (the workgroup holds the CU's LDS anyway)
+  asm volatile("" ::: "a255");
   const int t = threadIdx.x, wv = t >> 6, l = t & 63;
   const int n_traj = count ? *count : w.Bt;
   for (int jb = blockIdx.x; jb < n_traj; jb += gridDim.x) {  // uniform over the workgroup

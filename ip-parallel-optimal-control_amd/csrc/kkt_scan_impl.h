@@ -282,13 +282,16 @@ NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st, double reg) {
 // larger nx by threshold-checked Gaussian elimination without row exchanges, redone with partial
 // pivoting by the whole segment (uniform branch, so the re-fetch is legal) if any lane's check
 // fails.
-template <int NX, bool VALUE_ONLY, int SK>
+template <int NX, bool VALUE_ONLY, int SK, bool MASKED = (NX <= 2)>
 NOC_DEV void combine_sklansky(Elem<NX>& e1) {
   const int lane = (int)__lane_id();
   // MASKED: the arithmetic under EXEC = the combining lanes; else every lane computes, the others
-  // with the exact identity element as partner (which leaves them unchanged): nx = 4 elements
-  // are too large to keep old and new values apart across the branches without spilling
-  constexpr bool MASKED = NX <= 2;
+  // with the exact identity element as partner (which leaves them unchanged, at one select per
+  // fetched dword): at two waves per SIMD (256 registers) nx = 4 elements are too large to keep
+  // old and new values apart across the branches without spilling.  The two-wave segments (512
+  // registers) mask every nx: their phase 2 28.4 k -> 26.3 k cycles per wave (512-per-GPU shard);
+  // the wide persistent solver, whose cart-pole instance already keeps 116 values in AGPRs, was
+  // 1.5-2.5 % slower masked and keeps the selects (profiles/r03/two_wave/)
   const bool act = MASKED ? !(lane & (1 << SK)) : true;
   const bool comb = !(lane & (1 << SK));
   auto fetch = [&](double v, double idv) {
@@ -424,6 +427,67 @@ NOC_DEV double* lds_slots(int N) {
   const int per_traj = (N * kd_width<NX, NU>() + NX + 1) & ~1;
   return noc_smem + (size_t)(threadIdx.x / L) * per_traj;
 }
+// Two-wave segments (L = 128, one trajectory per 128-thread block): the cross-wave hand-offs go
+// through a small LDS region behind the slots (at 0 when the slots are not staged): the later
+// wave's value at its start (J, nu), the state at its start, the later wave's pred / feasibility.
+template <int NX>
+__host__ __device__ constexpr int join_doubles() { return ((NX * (NX + 1)) / 2 + 2 * NX + 2 + 1) & ~1; }
+template <int NX, int NU>
+NOC_DEV double* lds_join(int N, bool slots_staged) {
+  extern __shared__ __attribute__((aligned(16))) double noc_smem[];
+  return noc_smem + (slots_staged ? ((N * kd_width<NX, NU>() + NX + 1) & ~1) : 0);
+}
+
+// e1 <- e1 (x) (value-only e2 = (J2, nu2)): the true value function at e1's start given the value
+// at its end (the VALUE_ONLY branch of combine_sklansky with the partner given explicitly; the
+// cross-wave joins of the two-wave scan and of the wide persistent solver, ipm_wide.hip)
+template <int NX>
+NOC_DEV void apply_value(Elem<NX>& e1, const Sym<NX>& J2, const Vec<NX>& nu2) {
+  double X[NX][NX], Y[NX][NX];
+  auto build = [&]() {
+    NOC_UNROLL for (int i = 0; i < NX; ++i)
+      NOC_UNROLL for (int j = 0; j < NX; ++j) {
+        double s = (i == j) ? 1.0 : 0.0;
+        NOC_UNROLL for (int k = 0; k < NX; ++k) s += e1.C(i, k) * J2(k, j);
+        X[i][j] = s;
+        Y[i][j] = e1.A(i, j);
+      }
+  };
+  build();
+  Mat<NX, NX> J2A1;
+  Vec<NX> w;
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    double sw = nu2[i];
+    NOC_UNROLL for (int k = 0; k < NX; ++k) sw += J2(i, k) * e1.b[k];
+    w[i] = sw;
+    NOC_UNROLL for (int j = 0; j < NX; ++j) {
+      double s = 0.0;
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += J2(i, k) * e1.A(k, j);
+      J2A1(i, j) = s;
+    }
+  }
+  // nx = 2: closed form (det(I + C1 J2) >= 1), as combine_sklansky; else the threshold-checked
+  // elimination with a per-lane fallback (no shuffles here, so no uniformity is needed)
+  if constexpr (NX == 2) {
+    solve2_closed<NX>(X, Y);
+  } else if (!lu_np_solve<NX, NX>(X, Y)) {
+    build();
+    lu_pp_solve<NX, NX>(X, Y);
+  }
+  NOC_UNROLL for (int i = 0; i < NX; ++i) {
+    NOC_UNROLL for (int j = i; j < NX; ++j) {
+      double s = e1.J(i, j);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * J2A1(k, j);
+      e1.J(i, j) = s;
+    }
+    double s = e1.nu[i];
+    NOC_UNROLL for (int k = 0; k < NX; ++k) s += Y[k][i] * w[k];
+    e1.nu[i] = s;
+  }
+  set_zero(e1.A);
+  set_zero(e1.b);
+  set_zero(e1.C);
+}
 
 // Where the scan gets a stage's LQ blocks: from the KKTArgs arrays (tiled or natural layout).
 // The persistent solver passes a source that recomputes them from (x, u, lambda) instead.
@@ -467,6 +531,18 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   const double reg = a.reg ? a.reg[traj] : 0.0;
   const size_t tN = (size_t)traj * N;
   const int cmax = base + (rem ? 1 : 0);
+  // LW lanes of one wave in the segment, W waves per segment (W = 2: L = 128, the horizon split
+  // over the two waves of a 128-thread block; the wave-level scans run per wave and are joined
+  // through LDS -- for batches too small to give every SIMD a wave at L = 64)
+  constexpr int LW = L > 64 ? 64 : L;
+  constexpr int W = L / LW;
+  static_assert(W == 1 || W == 2, "segments of up to two waves");
+  const int wv = l / LW, lw = l % LW;
+  double* join = nullptr;
+  if constexpr (W > 1) join = lds_join<NX, NU>(N, a.lds_out != 0);
+  (void)wv;
+  (void)lw;
+  (void)join;
   NOC_STAMP(0);
   StageData<NX, NU> cache[CACHE > 0 ? CACHE : 1];
   if constexpr (CACHE > 0) {
@@ -516,8 +592,33 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     }
     NOC_STAMP(1); NOC_ISA_MARK("phase", 1);
     // ---------------- phase 2: reverse Sklansky scan across lanes ----------------
-    if (!(a.ablate & 1)) {
-      rev_scan_sklansky<NX, L>(e);
+    if constexpr (W == 1) {
+      if (!(a.ablate & 1)) rev_scan_sklansky<NX, L>(e);
+    } else {
+      if (!(a.ablate & 1)) {
+        // per wave; wave 1 ends at the terminal cost (value-only last level), wave 0 at wave 1's
+        // start (full last level: its elements are joined below)
+        combine_sklansky<NX, false, 0, true>(e);
+        combine_sklansky<NX, false, 1, true>(e);
+        combine_sklansky<NX, false, 2, true>(e);
+        combine_sklansky<NX, false, 3, true>(e);
+        combine_sklansky<NX, false, 4, true>(e);
+        if (wv == W - 1) combine_sklansky<NX, true, 5, true>(e);  // wave-uniform branch
+        else combine_sklansky<NX, false, 5, true>(e);
+      }
+      // join: wave 1's value at its start, applied to every lane of wave 0
+      if (wv == 1 && lw == 0) {
+        NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) join[i] = e.J.v[i];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) join[Sym<NX>::SZ + i] = e.nu.v[i];
+      }
+      __syncthreads();
+      if (wv == 0) {
+        Sym<NX> Jw;
+        Vec<NX> nw;
+        NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) Jw.v[i] = join[i];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) nw.v[i] = join[Sym<NX>::SZ + i];
+        apply_value<NX>(e, Jw, nw);
+      }
     }
     if (a.ablate & 4) {  // phase 1 (+2) only: keep the element alive, skip the rest
       if (a.pred) a.pred[traj] = e.J(0, 0) + e.A(0, 0) + e.C(0, 0) + e.nu[0] + e.b[0];
@@ -527,8 +628,14 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     // ---------------- phase 3: in-chunk Riccati from the true boundary ----------------
     Sym<NX> S;
     Vec<NX> v;
-    shfl_down_arr<Sym<NX>::SZ>(e.J.v, S.v, 1, L);
-    shfl_down_arr<NX>(e.nu.v, v.v, 1, L);
+    shfl_down_arr<Sym<NX>::SZ>(e.J.v, S.v, 1, LW);
+    shfl_down_arr<NX>(e.nu.v, v.v, 1, LW);
+    if constexpr (W > 1) {  // wave 0's last lane ends where wave 1 starts
+      if (wv == 0 && lw == LW - 1) {
+        NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) S.v[i] = join[i];
+        NOC_UNROLL for (int i = 0; i < NX; ++i) v.v[i] = join[Sym<NX>::SZ + i];
+      }
+    }
     if (last) {  // boundary of the last chunk: the terminal cost itself (reloaded, not kept live)
       gload_sym<NX>(a.P + (size_t)traj * NX * NX, S);
       set_zero(v);
@@ -678,7 +785,19 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       }
     }
     // segment reductions: pred = sum, feasible = and (VALU butterfly, small_linalg.h)
-    segment_sum_and<L>(pred, feas, (int)__lane_id());
+    segment_sum_and<LW>(pred, feas, (int)__lane_id());
+    if constexpr (W > 1) {  // wave 0's sum + wave 1's sum
+      constexpr int PO = Sym<NX>::SZ + 2 * NX;
+      if (wv == 1 && lw == 0) {
+        join[PO] = pred;
+        join[PO + 1] = feas ? 1.0 : 0.0;
+      }
+      __syncthreads();
+      if (l == 0) {
+        pred += join[PO];
+        feas &= join[PO + 1] != 0.0 ? 1 : 0;
+      }
+    }
     if (l == 0) {
       if (a.pred) a.pred[traj] = pred;
       if (a.feasible) a.feasible[traj] = feas;
@@ -735,10 +854,32 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     }
     set_zero(Phi);
   }
-  affine_prefix_sklansky<NX, L>(Phi, phi);  // partners on the VALU (small_linalg.h)
+  affine_prefix_sklansky<NX, LW>(Phi, phi);  // partners on the VALU (small_linalg.h)
   Vec<NX> x;
-  shfl_up_arr<NX>(phi.v, x.v, 1, L);
+  shfl_up_arr<NX>(phi.v, x.v, 1, LW);
   if (l == 0) x = x0;
+  if constexpr (W > 1) {
+    // wave 0's prefixes start from the constant map of lane 0, so its last one is the state at
+    // wave 1's start; wave 1 applies its own (non-constant) prefixes to it
+    constexpr int XO = Sym<NX>::SZ + NX;
+    if (wv == 0 && lw == LW - 1) NOC_UNROLL for (int i = 0; i < NX; ++i) join[XO + i] = phi[i];
+    Mat<NX, NX> oP;
+    if (wv == 1) shfl_up_arr<NX * NX>(Phi.v, oP.v, 1, LW);  // wave-uniform branch
+    __syncthreads();
+    if (wv == 1) {
+      Vec<NX> xw;
+      NOC_UNROLL for (int i = 0; i < NX; ++i) xw[i] = join[XO + i];
+      if (lw == 0) {
+        x = xw;
+      } else {
+        NOC_UNROLL for (int i = 0; i < NX; ++i) {
+          double t = x[i];
+          NOC_UNROLL for (int k = 0; k < NX; ++k) t += oP(i, k) * xw[k];
+          x[i] = t;
+        }
+      }
+    }
+  }
   NOC_STAMP(4); NOC_ISA_MARK("phase", 4);
   // dx/du rows go through LDS (slot s of the trajectory's region holds K_s, d_s from phase 3 and
   // is overwritten by x_s, u_s here) and leave as whole contiguous rows: per-lane direct stores
@@ -834,7 +975,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     return;
   }
   if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) slot[N * KD + i] = x[i];
-  __syncthreads();  // one wave per block: orders this wave's LDS writes before its reads
+  __syncthreads();  // orders the segment's LDS writes (one or two waves) before its reads
   if (a.dx) {
     double* dst = a.dx + (tN + traj) * NX;
     if constexpr (NX % 2 == 0) {
@@ -873,8 +1014,16 @@ NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
 }
 
 template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE>
-__global__ __launch_bounds__(64, NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
+__global__ __launch_bounds__(L > 64 ? L : 64, L > 64 ? 1 : NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  // Two-wave segments (L = 128) must put their two waves on DIFFERENT SIMDs: with <= 256
+  // registers per wave the dispatcher placed both waves of a 128-thread block on one SIMD (their
+  // combine levels then took turns on one VALU: phase 2 36.6 k vs 23.4 k cycles per wave,
+  // profiles/r03/shards/stamps_s512_L128.txt).  Claiming the whole register file (the AGPR half
+  // included: no wave of this kernel can share a SIMD) makes the two waves of a block land on two
+  // SIMDs; the launch policy (kkt_pick_lanes) uses L = 128 only when every wave is then resident
+  // at once (B * 2 <= #SIMDs).
+  if constexpr (L > 64) asm volatile("" ::: "a255");
   kkt_scan_wave<NX, NU, L, AFF, TILED, CACHE>(a, tid / L, tid % L);
 }
 
@@ -891,10 +1040,13 @@ template <int NX, int NU, int L, bool AFF>
 hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
   KKTArgs a = a_in;
   const long long threads = (long long)a.B * L;
-  const int block = 64;  // one wave per workgroup: waves are independent (no LDS sharing)
+  // one wave per workgroup (waves are independent: no LDS sharing); L = 128: one trajectory per
+  // two-wave workgroup (the waves join through LDS)
+  const int block = L > 64 ? L : 64;
   const unsigned grid = (unsigned)((threads + block - 1) / block);
-  const size_t lds = (a.mode == MODE_BWD || (!a.dx && !a.du)) ? 0 : kkt_lds_bytes_rt(NX, NU, a.N, L);
-  a.lds_out = lds > 0 ? 1 : 0;
+  const size_t slots = (a.mode == MODE_BWD || (!a.dx && !a.du)) ? 0 : kkt_lds_bytes_rt(NX, NU, a.N, L);
+  a.lds_out = slots > 0 ? 1 : 0;
+  const size_t lds = slots + (L > 64 ? join_doubles<NX>() * sizeof(double) : 0);
   if (!a.lds_out && (!a.K || !a.d)) return hipErrorInvalidValue;  // K/d needed as workspace
   constexpr int CC = kkt_cache_len<NX, NU, L>();
   const int cmax = a.N / L + (a.N % L ? 1 : 0);
@@ -916,6 +1068,9 @@ hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
 template <int NX, int NU, bool AFF>
 static hipError_t dispatch_lanes(const KKTArgs& a, int lanes, hipStream_t stream) {
   switch (lanes) {
+    case 128:  // two-wave segments: small nx only (nx = 8 batches use the group solve)
+      if constexpr (NX <= 4) return launch_kkt<NX, NU, 128, AFF>(a, stream);
+      else return hipErrorInvalidValue;
     case 64: return launch_kkt<NX, NU, 64, AFF>(a, stream);
     case 32: return launch_kkt<NX, NU, 32, AFF>(a, stream);
     case 16: return launch_kkt<NX, NU, 16, AFF>(a, stream);

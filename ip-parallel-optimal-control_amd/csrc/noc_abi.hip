@@ -42,8 +42,9 @@ int check_dims(int nx, int nu, int N, int B, int lanes) {
                         "); supported: " + noc::kkt_shapes_str());
   if (N < 1) return fail(-1, "horizon N must be >= 1");
   if (B < 0) return fail(-1, "batch B must be >= 0");
-  if (lanes != 0 && lanes != 1 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64)
-    return fail(-1, "lanes must be 0, 1, 8, 16, 32 or 64");
+  if (lanes != 0 && lanes != 1 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64 &&
+      lanes != 128)
+    return fail(-1, "lanes must be 0, 1, 8, 16, 32, 64 or 128");
   return 0;
 }
 }  // namespace
@@ -103,7 +104,8 @@ static int device_simds() {
 // >= cmin stages (the cross-lane combine is amortised over the chunk: nx = 2 needs 3, nx = 4 four;
 // shorter chunks are combine-bound, longer ones serialise the lane and, at L = 32 and N >= 300,
 // the on-chip gains cap residency at 6 waves/CU), then (2) double L while the batch gives fewer
-// waves than the device has SIMDs (a half-empty chip loses more than a short chunk costs).
+// waves than the device has SIMDs (a half-empty chip loses more than a short chunk costs), up to
+// two waves per trajectory.
 int kkt_pick_lanes(int nx, int nu, int N, int B) {
   if (nx >= 8) return kkt_default_lanes(nx, nu, N);
   const int cmin = nx <= 2 ? 3 : 4;
@@ -111,7 +113,12 @@ int kkt_pick_lanes(int nx, int nu, int N, int B) {
   for (int c = 64; c >= 8; c /= 2)
     if (N >= cmin * c) { L = c; break; }
   const long simds = device_simds();
-  while (L < 64 && (long)B * L < 64 * simds) L *= 2;
+  // (3) two waves per trajectory (L = 128, nx <= 4) only when the horizon gives every lane of
+  // both waves a stage and the whole batch is resident at once: that instance runs one wave per
+  // SIMD (kkt_scan_kernel), so B * 2 waves must not exceed the SIMDs
+  while ((long)B * L < 64 * simds &&
+         (L < 64 || (L == 64 && nx <= 4 && N >= 128 && (long)B * 2 <= simds)))
+    L *= 2;
   return L;
 }
 }  // namespace noc
@@ -222,8 +229,8 @@ int noc_relayout(int direction, int E, int sym_n, int N, int B, int lanes, const
                  double* dst, void* stream) {
   if (direction != 0 && direction != 1) return fail(-1, "direction must be 0 or 1");
   if (N < 1 || B < 0 || E < 1) return fail(-1, "bad dims");
-  if (lanes != 1 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64)
-    return fail(-1, "lanes must be 1/8/16/32/64");
+  if (lanes != 1 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64 && lanes != 128)
+    return fail(-1, "lanes must be 1/8/16/32/64/128");
   if (sym_n > 0 && E != sym_n * (sym_n + 1) / 2) return fail(-1, "E must be sym_n(sym_n+1)/2");
   if (!src || !dst) return fail(-2, "NULL pointer");
   return hip_status(noc::relayout(direction, E, sym_n, N, B, lanes, src, dst,

@@ -32,12 +32,14 @@ struct KKTArgs {
 
 // On-chip staging of the KKT scan (kkt_scan_impl.h): per trajectory N slots of nu*(nx+1) doubles
 // (K_s, d_s, later overwritten by dx_s, du_s) + dx_N, one region per L-lane segment of the
-// 64-thread block.  Staged when a block's region fits in 20 KB (8 resident waves per CU).
+// 64-thread block (L = 128: one per 128-thread block).  Staged when the region fits in 20 KB per
+// wave (8 resident waves per CU).
 inline size_t kkt_lds_bytes_rt(int nx, int nu, int N, int L) {
   if (L < 8) return 0;  // lanes = 1 (group solve): gains go through HBM
   const size_t per_traj = (size_t)(((long long)N * nu * (nx + 1) + nx + 1) & ~1LL);
-  const size_t bytes = (size_t)(64 / L) * per_traj * sizeof(double);
-  return bytes <= 20480 ? bytes : 0;
+  const size_t segs = L >= 64 ? 1 : 64 / L;  // trajectories per workgroup (L = 128: two waves)
+  const size_t bytes = segs * per_traj * sizeof(double);
+  return bytes <= 20480 * (size_t)(L > 64 ? L / 64 : 1) ? bytes : 0;
 }
 
 // Retry fixed point of the par inner loop (P:151-188).  A rejected trial whose rp was already at

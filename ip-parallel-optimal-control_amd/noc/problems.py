@@ -201,12 +201,20 @@ def make_bench_blocks(name: str, N: int, batch: int, seed: int = 0, device="cuda
     x0, u0 = initial_conditions(name, N, batch, seed)
     # one all-active KKT launch over the batch: the batch-aware lanes policy
     lanes = lanes or pick_lanes(ocp.family.nx, ocp.family.nu, N, batch)
-    eng = BatchedIPM(ocp.family, N, batch, device=device, lanes=lanes)
+    # the interior-point workspace's tiled layout spans one wave (lanes <= 64); two-wave segments
+    # (lanes = 128) get the same blocks relaid out on the device
+    eng = BatchedIPM(ocp.family, N, batch, device=device, lanes=min(lanes, 64))
     eng.load(u0, x0)
     eng.init(bp0=0.1)
     eng.prepare(mode=_lib.MODE_PAR, terminal=_lib.TERMINAL_FINAL_COST)
     t = eng.t
-    out = dict(tiled=eng.tiled_blocks(), reg=t["reg"], x=t["x"], u=t["u"], engine=eng)
+    if lanes == eng.lanes:
+        tiled = eng.tiled_blocks()
+    else:
+        from .lqt import to_tiled
+        nat = eng.natural_blocks()
+        tiled = to_tiled(*(nat[k] for k in ("A", "B", "Q", "R", "M", "r", "P")), lanes)
+    out = dict(tiled=tiled, reg=t["reg"], x=t["x"], u=t["u"], engine=eng)
     if natural:
         out.update(eng.natural_blocks())
     return out

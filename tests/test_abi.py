@@ -54,6 +54,9 @@ def test_batch_aware_lane_policy_picks_the_measured_best():
         (4, 1, 200, 4096): (32,), (4, 1, 300, 4096): (64,), (4, 1, 400, 4096): (64,),
         (4, 1, 200, 1024): (32, 64), (4, 1, 200, 16384): (32,),
         (2, 1, 100, 1024): (64,), (2, 1, 100, 4096): (32, 16), (2, 1, 100, 16384): (32,),
+        # round 3: the 8-GPU shard of the north-star curve, two waves per trajectory
+        # (profiles/r03/shards/)
+        (4, 1, 200, 512): (128,),
     }
     for (nx, nu, N, B), ok in cases.items():
         assert lib.noc_kkt_pick_lanes(nx, nu, N, B) in ok, (nx, nu, N, B)

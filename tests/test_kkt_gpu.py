@@ -37,11 +37,14 @@ def run_kkt(case, lanes, want_value=True):
 
 
 @pytest.mark.parametrize("nx,nu", [(2, 1), (4, 1), (8, 4)])
-@pytest.mark.parametrize("lanes", [64, 32, 16, 8, 1])
+@pytest.mark.parametrize("lanes", [128, 64, 32, 16, 8, 1])
 @pytest.mark.parametrize("N", [1, 7, 50, 200])
 @pytest.mark.parametrize("affine", [False, True])
 def test_kkt_matches_oracle(nx, nu, lanes, N, affine):
-    """lanes 64..8: parallel-in-time scan; lanes 1: horizon-sequential nx-lane group solve."""
+    """lanes 64..8: parallel-in-time scan in one wave; 128: two waves per trajectory joined
+    through LDS (nx <= 4); lanes 1: horizon-sequential nx-lane group solve."""
+    if lanes == 128 and nx == 8:
+        pytest.skip("two-wave segments are instantiated for nx <= 4 (test_two_wave_nx8_rejected)")
     case = rand_lq(1000 * nx + N + lanes + int(affine), 5, N, nx, nu, affine=affine)
     ref = oracle_batch(case)
     out = run_kkt(case, lanes)
@@ -51,19 +54,30 @@ def test_kkt_matches_oracle(nx, nu, lanes, N, affine):
     assert np.array_equal(out["feasible"].astype(bool), ref["feasible"].astype(bool))
 
 
-def test_kkt_infeasible_flag():
+def test_two_wave_nx8_rejected():
+    """lanes = 128 is not instantiated for nx = 8: an error, not a silent fallback."""
+    from noc import lqt, _lib
+    case = rand_lq(8, 2, 20, 8, 4)
+    g = lambda k: dev(case.get(k))
+    with pytest.raises(_lib.NocError):
+        lqt.kkt_solve(g("A"), g("B"), g("Q"), g("R"), g("M"), g("r"), g("P"), reg=g("reg"),
+                      lanes=128)
+
+
+@pytest.mark.parametrize("lanes", [64, 128])
+def test_kkt_infeasible_flag(lanes):
     case = rand_lq(7, 4, 30, 4, 1)
     case["R"][1, 10] = -50.0   # Quu < 0 at stage 10 of trajectory 1
     case["R"][3, 29] = -50.0
     ref = oracle_batch(case)
-    out = run_kkt(case, 64)
+    out = run_kkt(case, lanes)
     assert list(out["feasible"]) == [1, 0, 1, 0]
     assert list(ref["feasible"].astype(int)) == [1, 0, 1, 0]
     ok = [0, 2]
     assert relerr(out["dx"][ok], ref["dx"][ok]) < RTOL
 
 
-@pytest.mark.parametrize("lanes", [0, 1])
+@pytest.mark.parametrize("lanes", [0, 1, 128])
 def test_kkt_active_mask_leaves_inactive_untouched(lanes):
     from noc import lqt
     case = rand_lq(11, 6, 40, 4, 1)
@@ -88,10 +102,13 @@ def test_kkt_active_mask_leaves_inactive_untouched(lanes):
 
 
 @pytest.mark.parametrize("nx,nu", [(2, 1), (4, 1), (8, 4)])
-@pytest.mark.parametrize("bwd_lanes,fwd_lanes", [(16, 32), (1, 1), (1, 64), (8, 1)])
+@pytest.mark.parametrize("bwd_lanes,fwd_lanes", [(16, 32), (1, 1), (1, 64), (8, 1), (128, 64),
+                                               (64, 128), (128, 128)])
 def test_split_bwd_fwd_entry_points(nx, nu, bwd_lanes, fwd_lanes):
     """par_bwd_pass / par_fwd_pass split; the scan and the group solve interoperate through K, d."""
     from noc import lqt
+    if nx == 8 and 128 in (bwd_lanes, fwd_lanes):
+        pytest.skip("two-wave segments are instantiated for nx <= 4")
     case = rand_lq(5 + nx, 3, 37, nx, nu, affine=True)
     g = lambda k: dev(case.get(k))
     ref = oracle_batch(case)
@@ -142,7 +159,8 @@ def test_lqt_tracking_form_adapter():
 
 
 @pytest.mark.parametrize("nx,nu,lanes", [(nx, nu, L) for nx, nu in [(2, 1), (4, 1), (8, 4)]
-                                          for L in (64, 32, 16, 8)] + [(8, 4, 1)])
+                                          for L in (64, 32, 16, 8)] + [(8, 4, 1), (2, 1, 128),
+                                                                       (4, 1, 128)])
 @pytest.mark.parametrize("N", [1, 13, 200])
 def test_tiled_layout_kkt_matches_oracle(nx, nu, lanes, N):
     """The tiled layout the IPM workspace uses: lane-interleaved for the scan (lanes 8-64),
@@ -162,7 +180,7 @@ def test_tiled_layout_kkt_matches_oracle(nx, nu, lanes, N):
     assert np.array_equal(out.feasible.cpu().numpy().astype(bool), ref["feasible"].astype(bool))
 
 
-@pytest.mark.parametrize("lanes", [64, 16, 1])
+@pytest.mark.parametrize("lanes", [128, 64, 16, 1])
 def test_tile_untile_roundtrip(lanes):
     from noc import lqt
     rng = np.random.default_rng(0)
@@ -204,7 +222,8 @@ def test_cartpole_blocks_full_size_properties():
 
 
 @pytest.mark.parametrize("nx,nu,N,lanes", [(2, 1, 100, 64), (4, 1, 200, 32), (4, 1, 200, 64),
-                                           (4, 1, 50, 8), (8, 4, 40, 64)])
+                                           (4, 1, 50, 8), (8, 4, 40, 64), (4, 1, 200, 128),
+                                           (2, 1, 100, 128), (4, 1, 300, 128)])
 @pytest.mark.parametrize("affine", [False, True])
 def test_kkt_without_gains_matches_oracle(nx, nu, N, lanes, affine):
     """par_Newton's outputs only (want_gains=False): K, d stay in LDS between the backward and
@@ -223,7 +242,8 @@ def test_kkt_without_gains_matches_oracle(nx, nu, N, lanes, affine):
     assert np.array_equal(res.feasible.cpu().numpy().astype(bool), ref["feasible"].astype(bool))
 
 
-@pytest.mark.parametrize("N,lanes", [(64, 64), (100, 64), (128, 64), (64, 32), (65, 32)])
+@pytest.mark.parametrize("N,lanes", [(64, 64), (100, 64), (128, 64), (64, 32), (65, 32),
+                                     (100, 128), (256, 128), (257, 128)])
 @pytest.mark.parametrize("affine", [False, True])
 @pytest.mark.parametrize("gains", [False, True])
 def test_register_cached_chunk_equals_streamed(N, lanes, affine, gains):
@@ -282,13 +302,15 @@ def test_group_solve_linear8_blocks_properties():
 
 
 @pytest.mark.parametrize("name,N,B,lanes", [("linear8", 512, 16384, 1), ("cartpole", 200, 65536, 32),
-                                           ("pendulum", 100, 1024, 0), ("cartpole", 200, 4096, 0)])
+                                           ("pendulum", 100, 1024, 0), ("cartpole", 200, 4096, 0),
+                                           ("cartpole", 200, 512, 0)])
 def test_full_size_bench_blocks_properties(name, N, B, lanes):
     """The bench path at BASELINE full sizes where the oracle cannot run on every trajectory:
     c2 (pendulum, N=100, B=1024: the batch-aware pick = 64 lanes, register-cached chunks), c3
     (cart-pole, N=200, B=4096: 32 lanes), c4 (linear8, N=512, B=16384, group solve on the grouped
     layout) and c5's global batch on ONE GPU (cart-pole, N=200, B=65536 = 8 x 8192: 64-bit
-    indexing of the tiled layout).  Properties:
+    indexing of the tiled layout), and the 8-GPU shard of the north-star curve (cart-pole, N=200,
+    512 per GPU: the pick = 128 lanes, two waves per trajectory).  Properties:
     dx_{k+1} = A dx_k + B du_k on every trajectory, all feasible, finite pred, and oracle parity
     on a strided sample of 8 trajectories including the last one."""
     from noc import lqt
