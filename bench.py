@@ -382,6 +382,19 @@ def main():
         abytes = int(allreduce([abytes], "max")[0])
     achieved = abytes / (kern_ms * 1e-3) / 1e9
     traffic, traffic_note = pmc_traffic(args.pmc_json, f"{args.problem}_N{N}_B{B}")
+    # what limits the launch below the HBM roofline (DESIGN.md §3.1 stamps): with at most one
+    # wave per SIMD the per-wave dependent chain (combine levels, load latency) sets the time;
+    # above it the blocks' three passes (one from HBM, two from the memory-side cache)
+    simds = 4 * torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    waves = -(-B * lanes // 64) if lanes >= 8 else -(-B // 8)
+    if lanes < 8:
+        limiter = "hbm: two sweeps (blocks + gains), group solve"
+    elif waves <= simds:
+        limiter = (f"latency: {waves / simds:.2f} waves per SIMD, the per-wave chain of combine "
+                   "levels and load latencies, not bytes")
+    else:
+        limiter = (f"memory: {waves / simds:.2f} waves per SIMD; one HBM pass over the blocks and "
+                   "two re-reads served by the memory-side cache")
     result = {
         "metric": "KKT Newton-steps/sec at (horizon N x batch)",
         "value": value,
@@ -405,7 +418,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_note": traffic_note,
-                     "algorithmic_bytes_per_launch": abytes, "kernel_ms": kern_ms},
+                     "algorithmic_bytes_per_launch": abytes, "kernel_ms": kern_ms,
+                     "limiter": limiter},
         "rccl_world_size": dist.get_world_size() if world > 1 else 1,
         "process_group": (dist.get_backend() if world > 1 else None),
         "per_rank_kernel_ms": rank_kern_ms,

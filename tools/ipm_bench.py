@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """End-to-end batched interior-point solve timing (device loop), per-kernel breakdown via
 rocprofv3 when run under it.  Prints one JSON line."""
-import json, os, sys, time
+import hashlib, json, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ip-parallel-optimal-control_amd"))
 import numpy as np
@@ -35,4 +35,7 @@ print(json.dumps({"problem": name, "N": N, "B": B, "lanes": eng.lanes, "persiste
                   "mean_outer_iters": float(its.mean()), "max_kkt_solves": int(solves.max()),
                   "min_kkt_solves": int(solves.min()),
                   "repeats_accounted": int(eng.t["repeats"].sum().item()),
-                  "no_repeat_skip": bool(eng.ws.flags & _lib.WS_NO_REPEAT_SKIP)}))
+                  "no_repeat_skip": bool(eng.ws.flags & _lib.WS_NO_REPEAT_SKIP),
+                  # bit-identity across kernel variants (NOC_PERSIST_WAVES / NOC_PERSIST_QLDS)
+                  "u_sha1": hashlib.sha1(np.ascontiguousarray(U).tobytes()).hexdigest()[:16],
+                  "env": {k: v for k, v in os.environ.items() if k.startswith("NOC_")}}))
