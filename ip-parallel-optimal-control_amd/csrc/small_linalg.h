@@ -235,6 +235,20 @@ NOC_DEV double readlane_dbl(double v, int lane) {
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
   return __hiloint2double(hi, lo);
 }
+// Level-4 partner of the Sklansky scans (h = 16) without the SGPR round trip of v_readlane: the
+// xor-16 row of every lane by v_permlane16_swap (the pairing of segment_sum_and), then DPP
+// row_newbcast:RL of that row.  UPPER: rows 1 and 3 receive lane RL of rows 0 and 2 (forward scan,
+// RL = 15); else rows 0 and 2 receive lane RL of rows 1 and 3 (reverse scan, RL = 0).  The other
+// rows receive values they must not use.  Moves only: bit-exact.
+template <int RL, bool UPPER>
+NOC_DEV double permrow_bcast(double v) {
+  auto one = [](int x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    const int p = UPPER ? (int)r[0] : (int)r[1];
+    return __builtin_amdgcn_mov_dpp(p, 0x150 + RL, 0xF, 0xF, false);
+  };
+  return __hiloint2double(one(__double2hiint(v)), one(__double2loint(v)));
+}
 // Partner fetches of the Sklansky scans for the lanes that combine at level K (h = 2^K); the
 // other lanes receive some other lane's value, which they must not use (they skip the level's
 // arithmetic under EXEC).  Run at the segment's full EXEC: a DPP source lane must be active.
@@ -252,8 +266,7 @@ NOC_DEV double sklansky_fwd_fetch(double v, int lane) {
   } else if constexpr (K == 3) {
     return dpp_full<0x157>(v);                    // row_newbcast:7
   } else if constexpr (K == 4) {
-    const double a = readlane_dbl(v, 15), b = readlane_dbl(v, 47);
-    return (lane & 32) ? b : a;
+    return permrow_bcast<15, true>(v);            // lanes 16-31 <- 15, 48-63 <- 47
   } else {
     return readlane_dbl(v, 31);
   }
@@ -271,8 +284,7 @@ NOC_DEV double sklansky_rev_fetch(double v, int lane) {
   } else if constexpr (K == 3) {
     return dpp_full<0x158>(v);                    // row_newbcast:8
   } else if constexpr (K == 4) {
-    const double a = readlane_dbl(v, 16), b = readlane_dbl(v, 48);
-    return (lane & 32) ? b : a;
+    return permrow_bcast<0, false>(v);            // lanes 0-15 <- 16, 32-47 <- 48
   } else {
     return readlane_dbl(v, 32);
   }
