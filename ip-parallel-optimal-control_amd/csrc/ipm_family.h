@@ -247,9 +247,10 @@ NOC_DEV int resume_phase(int ph) {
   return ph;
 }
 
+// wave-wide sum, every lane the same value: the __shfl_xor butterfly (off = 32 .. 1) with VALU
+// partners (small_linalg.h: segment_allreduce), bit-identical to the shuffle loop
 NOC_DEV double wave_sum(double v) {
-  NOC_UNROLL for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+  return segment_allreduce<64>(v, (int)__lane_id(), [](double a, double b) { return a + b; });
 }
 
 }  // namespace noc

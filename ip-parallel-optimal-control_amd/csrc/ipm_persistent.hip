@@ -399,10 +399,12 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         // lambda at the chunk start := the scan's value g (not this lane's sweep): it is exactly the
         // boundary costate the previous lane used, so every consumer of lambda_k sees one value
         if (len > 0) gstore<NX>(LAM + (size_t)start * NX, g.v);
-        NOC_UNROLL for (int off = PL / 2; off > 0; off >>= 1) {
-          csum += __shfl_xor(csum, off, PL);
-          g2s += __shfl_xor(g2s, off, PL);
-          hmax = nan_max(hmax, __shfl_xor(hmax, off, PL));
+        {  // the __shfl_xor butterflies with VALU partners (bit-identical, small_linalg.h)
+          const int ln = (int)__lane_id();
+          auto add = [](double x, double y) { return x + y; };
+          csum = segment_allreduce<PL>(csum, ln, add);
+          g2s = segment_allreduce<PL>(g2s, ln, add);
+          hmax = segment_allreduce<PL>(hmax, ln, [](double x, double y) { return nan_max(x, y); });
         }
         if (terminal == NOC_TERMINAL_FINAL_COST && last) {  // hessian(final_cost) (S:66)
           double P[NX * NX];

@@ -315,6 +315,21 @@ NOC_DEV int xor_partner_i(int v, int lane) {
     return dpp_i<0xB1>(v);   // quad_perm [1, 0, 3, 2]
   }
 }
+// The same butterfly for one double with any commutative op (sum, nan-propagating max): every
+// lane of the segment ends with the value the __shfl_xor loop gives it -- bitwise, since each
+// step adds the pair (v_l, v_{l^off}) and a + b == b + a -- without the LDS round trips of
+// ds_bpermute (the interior-point solvers' wave reductions: trial cost, stage-cost sum, ||cu||,
+// max |Hu|).
+template <int L, class OP, int OFF = L / 2>
+NOC_DEV double segment_allreduce(double v, int lane, OP op) {
+  if constexpr (OFF >= 1) {
+    const int lo = xor_partner_i<OFF>(__double2loint(v), lane);
+    const int hi = xor_partner_i<OFF>(__double2hiint(v), lane);
+    return segment_allreduce<L, OP, OFF / 2>(op(v, __hiloint2double(hi, lo)), lane, op);
+  } else {
+    return v;
+  }
+}
 template <int L, int OFF = L / 2>
 NOC_DEV void segment_sum_and(double& sum, int& all, int lane) {
   if constexpr (OFF >= 1) {
