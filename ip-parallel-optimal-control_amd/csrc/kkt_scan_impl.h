@@ -628,8 +628,8 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     // ---------------- phase 3: in-chunk Riccati from the true boundary ----------------
     Sym<NX> S;
     Vec<NX> v;
-    shfl_down_arr<Sym<NX>::SZ>(e.J.v, S.v, 1, LW);
-    shfl_down_arr<NX>(e.nu.v, v.v, 1, LW);
+    wave_shift_down1<Sym<NX>::SZ>(e.J.v, S.v);  // lane l+1's value; the segment's last lane:
+    wave_shift_down1<NX>(e.nu.v, v.v);          // overwritten below (terminal / join)
     if constexpr (W > 1) {  // wave 0's last lane ends where wave 1 starts
       if (wv == 0 && lw == LW - 1) {
         NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) S.v[i] = join[i];
@@ -856,7 +856,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   }
   affine_prefix_sklansky<NX, LW>(Phi, phi);  // partners on the VALU (small_linalg.h)
   Vec<NX> x;
-  shfl_up_arr<NX>(phi.v, x.v, 1, LW);
+  wave_shift_up1<NX>(phi.v, x.v);  // lane l-1's prefix; segment starts: x0 / the join below
   if (l == 0) x = x0;
   if constexpr (W > 1) {
     // wave 0's prefixes start from the constant map of lane 0, so its last one is the state at
@@ -864,7 +864,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     constexpr int XO = Sym<NX>::SZ + NX;
     if (wv == 0 && lw == LW - 1) NOC_UNROLL for (int i = 0; i < NX; ++i) join[XO + i] = phi[i];
     Mat<NX, NX> oP;
-    if (wv == 1) shfl_up_arr<NX * NX>(Phi.v, oP.v, 1, LW);  // wave-uniform branch
+    if (wv == 1) wave_shift_up1<NX * NX>(Phi.v, oP.v);  // wave-uniform branch; lane 0 unused
     __syncthreads();
     if (wv == 1) {
       Vec<NX> xw;

@@ -212,6 +212,28 @@ NOC_DEV void shfl_up_arr(const double* src, double* dst, int d, int w) {
   NOC_UNROLL for (int i = 0; i < CNT; ++i) dst[i] = shfl_up_d(src[i], d, w);
 }
 
+// By-one lane shifts across the whole wave on the VALU (DPP wave_shl:1 / wave_shr:1) instead of
+// ds_bpermute: down, lane i <- lane i + 1; up, lane i <- lane i - 1; the wave's last (first) lane
+// receives 0.  For any segment width L this equals __shfl_down / __shfl_up(v, 1, L) on every lane
+// except each segment's last (first) lane -- which the KKT scan overwrites (terminal cost / x0 /
+// the two-wave joins) -- and moves bits only.
+template <int CNT>
+NOC_DEV void wave_shift_down1(const double* src, double* dst) {
+  NOC_UNROLL for (int i = 0; i < CNT; ++i) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(src[i]), 0x130, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(src[i]), 0x130, 0xF, 0xF, true);
+    dst[i] = __hiloint2double(hi, lo);
+  }
+}
+template <int CNT>
+NOC_DEV void wave_shift_up1(const double* src, double* dst) {
+  NOC_UNROLL for (int i = 0; i < CNT; ++i) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(src[i]), 0x138, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(src[i]), 0x138, 0xF, 0xF, true);
+    dst[i] = __hiloint2double(hi, lo);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Sklansky (tree) inclusive prefixes over an L-lane segment with partners fetched on the VALU
 // instead of through the LDS pipe (sklansky_*_fetch below; the scans: sklansky_fwd_level here,
