@@ -54,12 +54,6 @@ NOC_DEV IpmState* state_slot(int N) {
   return reinterpret_cast<IpmState*>(noc_smem + ((N * kd_width<NX, NU>() + NX + 1) & ~1));
 }
 
-// QLDS instances (SURVEY §8(f)1 at large batches, NOC_PERSIST_QLDS=1): the cost blocks Q, R, M, r
-// of the lane's chunk -- the fields phase 3 of the scan re-reads -- are also kept in LDS between
-// the block assembly and the scan, [chunk slot j][field e][lane] (a wave-wide access is 64
-// consecutive doubles: no bank conflicts); A, B still come from the workspace.
-template <int NX, int NU>
-constexpr int qlds_fields() { return Sym<NX>::SZ + Sym<NU>::SZ + NX * NU + NU; }
 // XLDS instances: the trajectory's states and controls x[0..N], u[0..N-1] live in LDS for the
 // whole solve (the rollout, linearisation, costate sweep, trial and update all read or write
 // them; from the workspace each access was a global round trip), copied in at the start and out
@@ -70,35 +64,7 @@ NOC_DEV constexpr int xlds_off(int N) {
 }
 template <int NX, int NU>
 NOC_DEV constexpr int xlds_doubles(int N) { return ((N + 1) * NX + N * NU + 1) & ~1; }
-template <int NX, int NU, bool XLDS>
-NOC_DEV double* qlds_base(int N) {
-  extern __shared__ __attribute__((aligned(16))) double noc_smem[];
-  return noc_smem + xlds_off<NX, NU>(N) + (XLDS ? xlds_doubles<NX, NU>(N) : 0);
-}
 
-// scan source of the QLDS instances: A, B from the tiled workspace, Q, R, M, r from LDS
-template <int NX, int NU, int L>
-struct QldsSrc {
-  const KKTArgs& a;
-  int traj, l, cmax;
-  size_t tN;
-  const double* q;  // qlds_base
-  NOC_DEV void stage(int s, int j, double reg, StageData<NX, NU>& st) const {
-    (void)s; (void)reg;
-    tload<NX * NX, L>(a.A, traj, j, l, cmax, st.A.v);
-    tload<NX * NU, L>(a.Bm, traj, j, l, cmax, st.B.v);
-    constexpr int E = qlds_fields<NX, NU>();
-    const double* p = q + (size_t)j * E * L + l;
-    int e = 0;
-    NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) st.Q.v[i] = p[(e++) * L];
-    NOC_UNROLL for (int i = 0; i < Sym<NU>::SZ; ++i) st.R.v[i] = p[(e++) * L];
-    NOC_UNROLL for (int i = 0; i < NX * NU; ++i) st.M.v[i] = p[(e++) * L];
-    NOC_UNROLL for (int i = 0; i < NU; ++i) st.r.v[i] = p[(e++) * L];
-  }
-  NOC_DEV void ab(int s, int j, Mat<NX, NX>& A, Mat<NX, NU>& Bm, Vec<NX>& c) const {
-    load_AB<NX, NU, L, false, true>(a, traj, tN + s, j, l, cmax, A, Bm, c);
-  }
-};
 }  // namespace
 
 #ifdef NOC_PERSIST_PROFILE
@@ -112,7 +78,7 @@ struct QldsSrc {
 // of scratch per lane at WPS = 2, none at WPS = 1), and which pays for the stage pairs below.
 // RESUME: continue from the workspace state (NOC_WS_RESUME; its own instance, so the plain solve's
 // register allocation does not carry the resume bookkeeping).
-template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS, bool QLDS = false>
+template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS>
 __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
                                                          int terminal, double bp0,
                                                          int max_solves) {
@@ -365,15 +331,6 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
           }
           tstore<NU, PL>(w.r, b, j, l, cmax, o.rr);
           gstore<NX>(LAM + (size_t)k * NX, o.lam);
-          if constexpr (QLDS) {  // the scan's copy (the workspace keeps its own for resumes)
-            constexpr int E = qlds_fields<NX, NU>();
-            double* p = qlds_base<NX, NU, XLDS>(N) + (size_t)j * E * PL + l;
-            int e = 0;
-            NOC_UNROLL for (int i = 0; i < Sym<NX>::SZ; ++i) p[(e++) * PL] = o.Qs.v[i];
-            NOC_UNROLL for (int i = 0; i < Sym<NU>::SZ; ++i) p[(e++) * PL] = o.Rs.v[i];
-            NOC_UNROLL for (int i = 0; i < NX * NU; ++i) p[(e++) * PL] = o.M[i];
-            NOC_UNROLL for (int i = 0; i < NU; ++i) p[(e++) * PL] = o.rr[i];
-          }
         };
         if (pair) {  // descending pairs over the wave-uniform chunk bound; short lanes skip slots
           for (int j = cmax - 1; j >= 0; j -= 2) {
@@ -432,12 +389,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       }
       // ---------------- KKT solve (par_Newton, P:107-124) ----------------
 #ifndef NOC_EXPT_NOKKT
-      if constexpr (QLDS) {
-        const QldsSrc<NX, NU, PL> src{a, b, l, cmax, (size_t)b * N, qlds_base<NX, NU, XLDS>(N)};
-        kkt_scan_wave_src<NX, NU, PL, false, true, QldsSrc<NX, NU, PL>, 0, false>(a, b, l, src);
-      } else {
-        kkt_scan_wave<NX, NU, PL, false, true, 0, false>(a, b, l);
-      }
+      kkt_scan_wave<NX, NU, PL, false, true, 0, false>(a, b, l);
 #endif
       wave_fence();  // pred / feasible written by lane 0
       {
@@ -597,10 +549,10 @@ static int device_simds() {
 template <int KIND>
 constexpr bool one_wave_instance() { return KIND == NOC_FAMILY_CARTPOLE; }
 
-template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS, bool QLDS = false>
+template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS>
 static hipError_t launch_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                                double bp0, int max_solves, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, WPS, RESUME, XLDS, QLDS>), dim3(w.Bt), dim3(64),
+  hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, WPS, RESUME, XLDS>), dim3(w.Bt), dim3(64),
                      lds, s, p, w, mode, terminal, bp0, max_solves);
   return hipGetLastError();
 }
@@ -611,18 +563,10 @@ static hipError_t solve_w(const noc_family& p, const noc_ipm_ws& w, int mode, in
   // x, u in LDS (XLDS) when that keeps the residency the register budget allows: 8 waves per CU
   // at 2 waves per SIMD (<= 20 KB per wave), 4 at one wave per SIMD (<= 40 KB); longer horizons
   // keep them in the workspace.  NOC_PERSIST_XLDS=0 forces the workspace (A/B).
-  static const char* xenv = getenv("NOC_PERSIST_XLDS");
+  const char* xenv = getenv("NOC_PERSIST_XLDS");  // per launch (tests switch it)
   const size_t xl = lds + (size_t)(((w.N + 1) * NX + w.N * NU + 1) & ~1) * sizeof(double);
   const bool xlds = !(xenv && atoi(xenv) == 0) && xl <= (WPS == 1 ? 40960u : 20480u);
   const bool res = (w.flags & NOC_WS_RESUME) != 0;
-  if constexpr (WPS == 1) {
-    // NOC_PERSIST_QLDS=1 (measurement instance): Q, R, M, r also kept in LDS for the
-    // scan; not for resumed launches (a SOLVE resume point has no LDS copy of the blocks)
-    static const char* qenv = getenv("NOC_PERSIST_QLDS");
-    const size_t ql = lds + (size_t)qlds_fields<NX, NU>() * ((w.N + PL - 1) / PL) * PL * sizeof(double);
-    if (qenv && atoi(qenv) == 1 && !res && ql <= 65536)
-      return launch_solve<KIND, NX, NU, 1, false, false, true>(p, w, mode, terminal, bp0, max_solves, ql, s);
-  }
   if (xlds)
     return res ? launch_solve<KIND, NX, NU, WPS, true, true>(p, w, mode, terminal, bp0, max_solves, xl, s)
                : launch_solve<KIND, NX, NU, WPS, false, true>(p, w, mode, terminal, bp0, max_solves, xl, s);

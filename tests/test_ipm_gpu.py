@@ -200,6 +200,34 @@ def test_persistent_solve_equals_multilaunch_loop(name, N, Bt, mode, monkeypatch
     assert np.max(np.abs(Up - Um)) <= 1e-12 * max(1.0, float(np.max(np.abs(Um))))
 
 
+@pytest.mark.parametrize("name,mode", [("pendulum", "par"), ("cartpole", "par"),
+                                       ("cartpole", "seq")])
+def test_persistent_states_in_lds_equal_workspace(name, mode, monkeypatch):
+    """The one-wave persistent solver with x, u resident in LDS for the whole solve (the default
+    where it fits) against the same solver on the workspace copies
+    (NOC_PERSIST_XLDS=0): the same arithmetic on the same values, so identical counters and
+    bit-identical controls and states; also across a capped launch and its resume."""
+    monkeypatch.setenv("NOC_PERSIST_WIDE", "0")
+    from noc import problems, _lib
+    from noc.ipm import BatchedIPM
+    N, Bt = 60, 48
+    ocp = problems.make_problem(name, N)
+    x0, u0 = problems.initial_conditions(name, N, Bt, seed=17)
+    m = _lib.MODE_PAR if mode == "par" else _lib.MODE_SEQ
+    res = []
+    for xlds in ("1", "0"):
+        monkeypatch.setenv("NOC_PERSIST_XLDS", xlds)
+        eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
+        eng.load(u0, x0)
+        eng.solve_persistent(mode=m, max_solves=40)      # capped mid-solve ...
+        eng.solve_persistent(mode=m, resume=True)        # ... and resumed to the end
+        torch.cuda.synchronize()
+        res.append([t.cpu().numpy() for t in eng.result()] + [eng.t["x"].cpu().numpy()])
+    (Ul, itl, sl, Xl), (Uw, itw, sw, Xw) = res
+    assert np.array_equal(itl, itw) and np.array_equal(sl, sw)
+    assert np.array_equal(Ul, Uw) and np.array_equal(Xl, Xw)
+
+
 @pytest.mark.parametrize("wide", ["0", "1"])
 def test_persistent_solve_respects_solve_cap(wide, monkeypatch):
     """A trajectory that reaches max_solves stops (phase != DONE) -- every wave exits (the one-wave
