@@ -54,9 +54,11 @@ def test_batch_aware_lane_policy_picks_the_measured_best():
         (4, 1, 200, 4096): (32,), (4, 1, 300, 4096): (64,), (4, 1, 400, 4096): (64,),
         (4, 1, 200, 1024): (32, 64), (4, 1, 200, 16384): (32,),
         (2, 1, 100, 1024): (64,), (2, 1, 100, 4096): (32, 16), (2, 1, 100, 16384): (32,),
-        # round 3: the 8-GPU shard of the north-star curve, two waves per trajectory
-        # (profiles/r03/shards/)
-        (4, 1, 200, 512): (128,),
+        # round 3: the 8-GPU shard of the north-star curve, two waves per trajectory, one wave
+        # per SIMD (profiles/r03/two_wave/: 25.7 vs 27.3 us at 64 lanes); the 2-GPU shard keeps 32
+        # lanes (profiles/r03/lanes2048/: 53.4 vs 59.2 us at 64); two-wave segments only while the
+        # whole batch is resident at one wave per SIMD (B * 2 <= 1024 SIMDs)
+        (4, 1, 200, 512): (128,), (4, 1, 200, 2048): (32,), (4, 1, 200, 600): (64,),
     }
     for (nx, nu, N, B), ok in cases.items():
         assert lib.noc_kkt_pick_lanes(nx, nu, N, B) in ok, (nx, nu, N, B)
