@@ -139,6 +139,12 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
   long long t_prev = clock64();
   if (l == 0 && b < kTrajStamps) g_traj_times[b][0] = (long long)__builtin_amdgcn_s_memrealtime();
 #endif
+  // lc_fresh: the workspace's stage costs (w.lc) already belong to the current (x, u) -- the last
+  // trial wrote them, and it was taken -- so the next linearisation skips f.stage_cost (the
+  // trial evaluated the same function on the same doubles: x + dx is the update's own sum).  False
+  // at every launch start (a resume may follow the per-phase driver, whose trial does not write
+  // w.lc) and after every rollout (new barrier parameter).
+  bool lc_fresh = false;
   for (;;) {  // ---------------- barrier stages (P:228-254) ----------------
     // rollout x_{k+1} = f(x_k, u_k) (noc/utils.py:57-63, P:133): every lane runs the recurrence
     // redundantly with u_k broadcast by readlane; lane t stores the states of block step t
@@ -168,6 +174,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
     }
     wave_fence();  // states of every stage visible to their chunk owners
     NOC_PHASE(0);
+    lc_fresh = false;
     bool relinearize = !RESUME || entry != NOC_PHASE_SOLVE;  // SOLVE: the ws blocks are current
     if constexpr (RESUME) entry = NOC_PHASE_ROLLOUT;
     bool stage_done = false;
@@ -180,14 +187,14 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         auto lin_compute = [&](const double* x, const double* u, LinOut& o) {
           f.jac(x, u, o.fx, o.fu);
           f.stage_grad(x, u, bp, o.cx, o.cu);
-          o.lc = f.stage_cost(x, u, bp);
+          if (!lc_fresh) o.lc = f.stage_cost(x, u, bp);  // uniform over the wave
         };
         auto lin_store = [&](int j, const LinOut& o) {
           tstore<NX * NX, PL>(w.A, b, j, l, cmax, o.fx);
           tstore<NX * NU, PL>(w.B, b, j, l, cmax, o.fu);
           tstore<NX, PL>(w.cx, b, j, l, cmax, o.cx);
           tstore<NU, PL>(w.cu, b, j, l, cmax, o.cu);
-          tstore<1, PL>(w.lc, b, j, l, cmax, &o.lc);
+          if (!lc_fresh) tstore<1, PL>(w.lc, b, j, l, cmax, &o.lc);
         };
         auto load_xu = [&](int k, double* x, double* u) {
           gload<NX>(X + (size_t)k * NX, x);
@@ -415,15 +422,17 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
           const double c0 = f.stage_cost(xt0, ut0, bp);
           const double c1 = f.stage_cost(xt1, ut1, bp);
           const bool f0 = f.feasible(xt0, ut0), f1 = f.feasible(xt1, ut1);
-          if (j < len) { ok &= f0 ? 1 : 0; tsum += c0; }
-          if (j + 1 < len) { ok &= f1 ? 1 : 0; tsum += c1; }
+          if (j < len) { ok &= f0 ? 1 : 0; tsum += c0; tstore<1, PL>(w.lc, b, j, l, cmax, &c0); }
+          if (j + 1 < len) { ok &= f1 ? 1 : 0; tsum += c1; tstore<1, PL>(w.lc, b, j + 1, l, cmax, &c1); }
         }
       } else {
         for (int j = 0; j < len; ++j) {
           double xt[NX], ut[NU];
           trial_load(start + j, xt, ut);
           ok &= f.feasible(xt, ut) ? 1 : 0;
-          tsum += f.stage_cost(xt, ut, bp);
+          const double c = f.stage_cost(xt, ut, bp);
+          tsum += c;
+          tstore<1, PL>(w.lc, b, j, l, cmax, &c);  // the next linearisation's, if taken
         }
       }
       if (last) {
@@ -472,6 +481,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         }
         if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) X[(size_t)N * NX + i] += slot[N * KD + i];
       }
+      lc_fresh = take;  // uniform; the trial stored this point's stage costs in w.lc
       __syncthreads();  // the next KKT solve overwrites the LDS slots read above
       NOC_PHASE(4);
 #ifdef NOC_PERSIST_PROFILE
