@@ -158,10 +158,10 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
   auto wg_reduce = [&](double* v, int n, const bool* is_max) {
     NOC_UNROLL for (int k = 0; k < 4; ++k) {
       if (k < n) {
-        NOC_UNROLL for (int off = 32; off > 0; off >>= 1) {
-          const double o = __shfl_xor(v[k], off, 64);
-          v[k] = is_max[k] ? nan_max(v[k], o) : v[k] + o;
-        }
+        // VALU butterfly (small_linalg.h), bit-identical to the __shfl_xor loop
+        const double r = v[k];
+        v[k] = is_max[k] ? segment_allreduce<64>(r, l, [](double x, double y) { return nan_max(x, y); })
+                         : segment_allreduce<64>(r, l, [](double x, double y) { return x + y; });
       }
     }
     __syncthreads();
@@ -315,8 +315,8 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
         // this lane's chunk-end costate: lane l+1's in-wave map applied to lw (lane 63: lw)
         Mat<NX, NX> Gd;
         Vec<NX> gd;
-        shfl_down_arr<NX * NX>(G.v, Gd.v, 1, 64);
-        shfl_down_arr<NX>(g.v, gd.v, 1, 64);
+        wave_shift_down1<NX * NX>(G.v, Gd.v);  // DPP; lane 63 uses lw below
+        wave_shift_down1<NX>(g.v, gd.v);
         double lam[NX];
         NOC_UNROLL for (int i = 0; i < NX; ++i) {
           double a = gd[i];
@@ -442,8 +442,8 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
       // lane 63: the next wave's; the horizon's last lane: the terminal cost)
       Sym<NX> S;
       Vec<NX> v;
-      shfl_down_arr<Sym<NX>::SZ>(e.J.v, S.v, 1, 64);
-      shfl_down_arr<NX>(e.nu.v, v.v, 1, 64);
+      wave_shift_down1<Sym<NX>::SZ>(e.J.v, S.v);  // DPP; lane 63: the next wave's value below
+      wave_shift_down1<NX>(e.nu.v, v.v);
       if (l == 63) { S = Jw; v = nw; }
       if (last) { S = Pt; set_zero(v); }
       Mat<NX, NX> Phi;
@@ -559,27 +559,8 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
       const bool bwd_ok = kred[1] != 0.0;
       // phase 4: forward affine scan from dx_0 = 0 (P:121-123); thread 0's map is constant
       if (t == 0) set_zero(Phi);
-#pragma unroll 1
-      for (int d = 1; d < 64; d <<= 1) {
-        Mat<NX, NX> oP;
-        Vec<NX> op;
-        shfl_up_arr<NX * NX>(Phi.v, oP.v, d, 64);
-        shfl_up_arr<NX>(phi.v, op.v, d, 64);
-        if (l >= d) {
-          Mat<NX, NX> Pn;
-          NOC_UNROLL for (int i = 0; i < NX; ++i) {
-            double a = phi[i];
-            NOC_UNROLL for (int k = 0; k < NX; ++k) a += Phi(i, k) * op[k];
-            phi[i] = a;
-            NOC_UNROLL for (int j = 0; j < NX; ++j) {
-              double c = 0.0;
-              NOC_UNROLL for (int k = 0; k < NX; ++k) c += Phi(i, k) * oP(k, j);
-              Pn(i, j) = c;
-            }
-          }
-          Phi = Pn;
-        }
-      }
+      // in-wave inclusive prefix of the chunk maps: Sklansky with VALU partners (small_linalg.h)
+      affine_prefix_sklansky<NX, 64>(Phi, phi);
       __syncthreads();  // aggregate slots (read by the backward join above)
       if (l == 63) {
         NOC_UNROLL for (int i = 0; i < NX * NX; ++i) sagg[wv * 64 + i] = Phi.v[i];
@@ -601,8 +582,8 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
       {
         Mat<NX, NX> oP;
         Vec<NX> op;
-        shfl_up_arr<NX * NX>(Phi.v, oP.v, 1, 64);
-        shfl_up_arr<NX>(phi.v, op.v, 1, 64);
+        wave_shift_up1<NX * NX>(Phi.v, oP.v);  // DPP; lane 0 uses xw
+        wave_shift_up1<NX>(phi.v, op.v);
         NOC_UNROLL for (int i = 0; i < NX; ++i) {
           double a = op[i];
           NOC_UNROLL for (int k = 0; k < NX; ++k) a += oP(i, k) * xw[k];
