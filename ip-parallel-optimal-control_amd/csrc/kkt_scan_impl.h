@@ -417,7 +417,7 @@ NOC_DEV void rev_scan_sklansky(Elem<NX>& e) {
   }
 }
 
-// On-chip slot region of one trajectory (one per L-lane segment of the 64-thread block): N slots
+// On-chip slot region of one trajectory (one per L-lane segment of the workgroup): N slots
 // of KD = NU*(NX+1) doubles (K_s, d_s after phase 3, then x_s, u_s in phase 4) + x_N.
 template <int NX, int NU>
 NOC_DEV constexpr int kd_width() { return NU * (NX + 1); }
@@ -1014,7 +1014,7 @@ NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
 }
 
 template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE>
-__global__ __launch_bounds__(L > 64 ? L : 64, L > 64 ? 1 : NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
+__global__ __launch_bounds__(L > 64 ? L : 256, L > 64 ? 1 : NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   // Two-wave segments (L = 128) must put their two waves on DIFFERENT SIMDs: with <= 256
   // registers per wave the dispatcher placed both waves of a 128-thread block on one SIMD (their
@@ -1040,11 +1040,13 @@ template <int NX, int NU, int L, bool AFF>
 hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
   KKTArgs a = a_in;
   const long long threads = (long long)a.B * L;
-  // one wave per workgroup (waves are independent: no LDS sharing); L = 128: one trajectory per
-  // two-wave workgroup (the waves join through LDS)
-  const int block = L > 64 ? L : 64;
+  // L <= 64: wpb independent waves per workgroup (no LDS sharing; each its own slot region);
+  // L = 128: one trajectory per two-wave workgroup (the waves join through LDS)
+  const size_t slots1 = (a.mode == MODE_BWD || (!a.dx && !a.du)) ? 0 : kkt_lds_bytes_rt(NX, NU, a.N, L);
+  const int wpb = L > 64 ? 1 : kkt_waves_per_block((threads + 63) / 64, slots1);
+  const int block = L > 64 ? L : 64 * wpb;
   const unsigned grid = (unsigned)((threads + block - 1) / block);
-  const size_t slots = (a.mode == MODE_BWD || (!a.dx && !a.du)) ? 0 : kkt_lds_bytes_rt(NX, NU, a.N, L);
+  const size_t slots = slots1 * wpb;
   a.lds_out = slots > 0 ? 1 : 0;
   const size_t lds = slots + (L > 64 ? join_doubles<NX>() * sizeof(double) : 0);
   if (!a.lds_out && (!a.K || !a.d)) return hipErrorInvalidValue;  // K/d needed as workspace

@@ -84,20 +84,6 @@ int kkt_default_lanes(int nx, int nu, int N) {
   return N >= 160 ? 32 : 64;
 }
 
-// SIMDs of the current device (4 per CU); 1024 (MI355X: 256 CUs) when no device is visible.
-static int device_simds() {
-  static int simds = 0;
-  if (simds == 0) {
-    int n = 0, dev = 0, cus = 0;
-    if (hipGetDeviceCount(&n) == hipSuccess && n > 0 && hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-      simds = 4 * cus;
-    else
-      simds = 1024;
-    (void)hipGetLastError();
-  }
-  return simds;
-}
 
 // Batch-aware lanes per trajectory (the measured lanes x horizon x batch sweep,
 // profiles/r01/session4/lanes_policy/): (1) the longest-parallel split whose chunks still hold
@@ -112,7 +98,7 @@ int kkt_pick_lanes(int nx, int nu, int N, int B) {
   int L = 8;
   for (int c = 64; c >= 8; c /= 2)
     if (N >= cmin * c) { L = c; break; }
-  const long simds = device_simds();
+  const long simds = kkt_device_simds();
   // (3) two waves per trajectory (L = 128, nx <= 4) only when the horizon gives every lane of
   // both waves a stage and the whole batch is resident at once: that instance runs one wave per
   // SIMD (kkt_scan_kernel), so B * 2 waves must not exceed the SIMDs

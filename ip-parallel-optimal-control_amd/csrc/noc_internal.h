@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "../../include/noc_hip.h"
 
 // The family / KKT-shape lists the dispatchers expand (X-macros).  A custom-family build points
@@ -34,6 +36,37 @@ struct KKTArgs {
 // (K_s, d_s, later overwritten by dx_s, du_s) + dx_N, one region per L-lane segment of the
 // 64-thread block (L = 128: one per 128-thread block).  Staged when the region fits in 20 KB per
 // wave (8 resident waves per CU).
+// SIMDs of the current device (4 per CU); 1024 (MI355X: 256 CUs) when no device is visible.
+inline int kkt_device_simds() {
+  static int simds = 0;
+  if (simds == 0) {
+    int n = 0, dev = 0, cus = 0;
+    if (hipGetDeviceCount(&n) == hipSuccess && n > 0 && hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+      simds = 4 * cus;
+    else
+      simds = 1024;
+    (void)hipGetLastError();
+  }
+  return simds;
+}
+
+// Independent waves per workgroup of the L <= 64 scan (the measured A/B,
+// profiles/r03/waves_per_block/): four while the batch's waves fit one per SIMD (fewer workgroups
+// to place: c2 7.98 -> 7.73 us), two beyond (c3 90.4 -> 89.0 us; two-wave groups at one wave per
+// SIMD were slower: c2 9.9 us).  NOC_KKT_WPB = 1 | 2 | 4 overrides (read once); capped so a
+// workgroup's on-chip slots stay within 64 KB.
+inline int kkt_waves_per_block(long waves, size_t lds_per_wave) {
+  static const int forced = [] {
+    const char* e = std::getenv("NOC_KKT_WPB");
+    const int v = e ? std::atoi(e) : 0;
+    return (v == 1 || v == 2 || v == 4) ? v : 0;
+  }();
+  int w = forced ? forced : (waves <= kkt_device_simds() ? 4 : 2);
+  while (w > 1 && lds_per_wave * w > 65536) w /= 2;
+  return w;
+}
+
 inline size_t kkt_lds_bytes_rt(int nx, int nu, int N, int L) {
   if (L < 8) return 0;  // lanes = 1 (group solve): gains go through HBM
   const size_t per_traj = (size_t)(((long long)N * nu * (nx + 1) + nx + 1) & ~1LL);
