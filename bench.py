@@ -124,13 +124,15 @@ def allreduce(vals, op="sum"):
     return t.tolist()
 
 
-def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
+def ipm_solve_rate(problem, N, B, rank, world, G, lo, seed=11):
     """End-to-end: the whole interior-point solve (P:228-254) of this rank's B trajectories with
     the persistent kernel (noc_ipm_solve, one launch), timed with HIP events; over ranks the wall
     time is the max and the solve counts are summed.  Reported beside the KKT metric:
     kkt_solves_per_s = KKT solves actually COMPUTED / wall time (the identical retries at the rp
     clip that are accounted without recomputation, ws.repeats, are excluded;
-    kkt_solves_reference_equivalent_per_s counts them as the reference would)."""
+    kkt_solves_reference_equivalent_per_s counts them as the reference would).  The rank solves
+    trajectories lo..lo+B-1 of ONE global batch of G (shard_initial_conditions), so the summed
+    counts of N ranks are those of the 1-rank solve of the same G trajectories."""
     import torch
     import torch.distributed as dist
     from noc import problems
@@ -142,7 +144,7 @@ def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
         # interior-point loop), so its KKT line is already the end-to-end step
         return {"skipped": "no persistent instance for this family / horizon (c4 is LQ-only in "
                            "the reference: one KKT solve per MPC step, LM:67-84)"}
-    x0, u0 = problems.initial_conditions(problem, N, B, seed=seed_base + rank)
+    x0, u0 = problems.shard_initial_conditions(problem, N, G, lo, lo + B, seed=seed)
     eng = BatchedIPM(ocp.family, N, B, persistent=True)
     eng.load(u0, x0)
     eng.solve(max_steps=8)  # warm-up
@@ -194,6 +196,20 @@ def ipm_solve_rate(problem, N, B, rank, world, seed_base=11):
             "converged": int(tot[1])}
 
 
+BENCH_SEED = 1234  # the global batch's seed (the same on every rank)
+
+
+def rank_shard(args, world, rank):
+    """(B, G, lo, scaling): this rank's trajectories lo..lo+B-1 of the global batch G.  Strong
+    scaling (default): G = --global-batch split by noc.distributed.shard_bounds; weak (--batch B):
+    G = B x world, rank r owning [rB, (r+1)B)."""
+    if args.batch is not None:
+        return args.batch, args.batch * world, rank * args.batch, "weak"
+    from noc.distributed import shard_bounds
+    lo, hi = shard_bounds(args.global_batch, world, rank)
+    return hi - lo, args.global_batch, lo, "strong"
+
+
 def free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
@@ -218,6 +234,14 @@ def dry_run_line(args, world, rank):
     """NOC_BENCH_DRYRUN=1 (CPU tests): the launcher, process group, max-over-ranks timing and the
     JSON assembly, with no GPU work -- value is null, so it can never pass for a measurement."""
     import torch.distributed as dist
+    from noc import problems
+    B, G, lo, scaling = rank_shard(args, world, rank)
+    x0, u0 = problems.shard_initial_conditions(args.problem, args.horizon, G, lo, lo + B,
+                                               seed=BENCH_SEED)
+    dump = os.environ.get("NOC_BENCH_DRYRUN_DUMP")
+    if dump:  # this rank's inputs, for the CPU test that they are a slice of the 1-rank inputs
+        import numpy as np
+        np.savez(os.path.join(dump, f"rank{rank}_of{world}.npz"), x0=x0, u0=u0, lo=lo, G=G)
     if world > 1:
         dist.barrier()
     t = [0.0]
@@ -230,7 +254,8 @@ def dry_run_line(args, world, rank):
             "unit": "trajectory-KKT-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,
             "dry_run": True, "data": "dry run: no GPU work (launcher / process-group rehearsal)",
-            "rccl_world_size": world, "ranks_seen": [int(r) for r in ranks]}
+            "rccl_world_size": world, "ranks_seen": [int(r) for r in ranks],
+            "scaling": scaling, "config": {"global_batch": G, "batch_per_gpu": B}}
 
 
 def allgather_float(v):
@@ -305,17 +330,14 @@ def main():
     from noc import lqt, problems, _lib
 
     N = args.horizon
-    if args.batch is not None:        # weak scaling: every rank owns --batch trajectories
-        B, G, scaling = args.batch, args.batch * world, "weak"
-    else:                             # strong scaling: the global batch is sharded
-        from noc.distributed import shard_bounds
-        lo, hi = shard_bounds(args.global_batch, world, rank)
-        B, G, scaling = hi - lo, args.global_batch, "strong"
+    B, G, lo, scaling = rank_shard(args, world, rank)
     # lanes 8..64: the parallel-in-time scan on the lane-interleaved layout; lanes 1: the
     # horizon-sequential group solve on the grouped layout (the nx = 8 default).  Either way the
-    # blocks are what the device linearisation writes for that solver.
-    blocks = problems.make_bench_blocks(args.problem, N=N, batch=B, seed=1234 + rank,
-                                        lanes=args.lanes, natural=(args.layout == "natural"))
+    # blocks are what the device linearisation writes for that solver.  Every rank linearises its
+    # slice of ONE global batch (one seed), so N ranks solve exactly the 1-rank problem.
+    blocks = problems.make_bench_blocks(args.problem, N=N, batch=B, seed=BENCH_SEED,
+                                        lanes=args.lanes, natural=(args.layout == "natural"),
+                                        shard=(G, lo))
     tb = blocks["tiled"]
     nx, nu, lanes = tb.nx, tb.nu, tb.lanes
     if args.layout == "tiled":
@@ -427,7 +449,7 @@ def main():
         "launch": "eager" if graph is None else "hip_graph (the K timed steps captured once, one replay)",
     }
     if not args.no_ipm:
-        result["ipm_solve"] = ipm_solve_rate(args.problem, N, B, rank, world)
+        result["ipm_solve"] = ipm_solve_rate(args.problem, N, B, rank, world, G, lo)
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             sample = min(args.cpu_sample, B)

@@ -260,6 +260,14 @@ int noc_lqr_params(int nx, int nu, int N, int B, const double* lam, const double
                    const double* fxx, const double* fuu, const double* fxu, double* ru, double* Q,
                    double* R, double* M, void* stream);
 
+/* check_traj_feasibility (noc/par_interior_point_newton.py:45-47) == check_feasibility
+ * (noc/seq_interior_point_newton.py:93-95): feasible[b] = all_k constraints(x_k, u_k) <= 0 over
+ * k < N, with the family's whole constraint vector (the built-ins' box on u; a registered family's
+ * own constraints(x, u), state constraints included).  x (B, N+1, nx), u (B, N, nu), feasible (B)
+ * int32 (1 / 0; a NaN entry is infeasible).  One wave64 per trajectory. */
+int noc_check_feasibility(const noc_family* fam, int N, int B, const double* x, const double* u,
+                          int* feasible, void* stream);
+
 /* Interior-point DDP (noc/differential_dynamic_programming.py: interior_point_ddp, D:189-208):
  * the whole barrier schedule of DDP iterations (second-order backward pass with the Vx . fxx
  * terms, nonlinear closed-loop rollout, retry loop) of every trajectory in ONE launch, one wave64

@@ -111,6 +111,41 @@ hipError_t final_cost_derivs(const noc_family& p, int B, const double* xN, doubl
 }
 
 // ------------------------------------------------------------------------------------------------
+// check_traj_feasibility (P:45-47) / check_feasibility (S:93-95): all(constraints(x_k, u_k) <= 0)
+// over k < N -- the family's whole constraint vector (the u box of the built-ins, a registered
+// family's traced constraints(x, u) incl. state constraints; NaN compares false, as jnp's <= does).
+// One wave64 per trajectory, lanes stride the stages, the verdict is the wave's vote.
+template <int KIND, int NX, int NU>
+__global__ __launch_bounds__(64) void feasibility_kernel(noc_family prm, int N, int B,
+                                                         const double* x, const double* u, int* ok) {
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  Fam<KIND, NX, NU> f(prm);
+  bool good = true;
+  for (int k = threadIdx.x; k < N; k += 64) {
+    double xk[NX], uk[NU];
+    NOC_UNROLL for (int i = 0; i < NX; ++i) xk[i] = x[((size_t)b * (N + 1) + k) * NX + i];
+    NOC_UNROLL for (int j = 0; j < NU; ++j) uk[j] = u[((size_t)b * N + k) * NU + j];
+    good = good && f.feasible(xk, uk);
+  }
+  const bool all = __all(good);
+  if (threadIdx.x == 0) ok[b] = all ? 1 : 0;
+}
+
+hipError_t traj_feasibility(const noc_family& p, int N, int B, const double* x, const double* u,
+                            int* ok, hipStream_t s) {
+#define NOC_FAMILY(K, X, U)                                                                   \
+  if (p.kind == K && p.nx == X && p.nu == U) {                                                \
+    hipLaunchKernelGGL((feasibility_kernel<K, X, U>), dim3(B), dim3(64), 0, s, p, N, B, x, u, \
+                       ok);                                                                   \
+    return hipGetLastError();                                                                 \
+  }
+#include NOC_FAMILIES_DEF
+#undef NOC_FAMILY
+  return hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------------------
 // costates lambda_k = cx_k + fx_k' lambda_{k+1} (C:43-54), lambda_N = lamT.
 // sequential (seq_costates, lax.scan): one thread per trajectory, the recurrence in stage order.
 template <int NX>

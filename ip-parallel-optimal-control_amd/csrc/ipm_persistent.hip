@@ -395,9 +395,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         st->it = it; st->inner = inner; st->total_it = total_it; st->solves = solves;
       }
       // ---------------- KKT solve (par_Newton, P:107-124) ----------------
-#ifndef NOC_EXPT_NOKKT
       kkt_scan_wave<NX, NU, PL, false, true, 0, false>(a, b, l);
-#endif
       wave_fence();  // pred / feasible written by lane 0
       {
         const IpmState* st = state_slot<NX, NU>(N);

@@ -12,7 +12,7 @@
 // 8 groups fall into different bank quarters (2-way instead of 8-way conflicts).
 // Contract of this path: Q and R are read through their upper triangle (lane q forms S_new[:, q]
 // from column q; the gathered S keeps entries i <= j), i.e. they are taken as symmetric.
-// The forward sweep keeps NOC_G8_FWD_DEPTH stages of its row loads in flight in registers.
+// The forward sweep keeps kFwdDepth stages of its row loads in flight in registers.
 // Two input layouts: natural (the ABI's [b][k][...]; each trajectory's 512/256/128 B blocks are
 // N*sz apart) and grouped (tiled with lanes = 1, small_linalg.h group_base: the wave's 8
 // trajectories of one stage contiguous per field, Q/R packed) -- what the IPM linearisation writes
@@ -68,20 +68,8 @@ NOC_DEV void glds16(const char* src, char* lds_dst) {
   __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)lds_dst, 16, 0, 0);
 }
 
-#ifndef NOC_G8_DPP
-#define NOC_G8_DPP 1
-#endif
-// stages of the forward sweep's loads in flight per wave (fused kernel / forward-only launch)
-#ifndef NOC_G8_FWD_DEPTH
-#define NOC_G8_FWD_DEPTH 2
-#endif
-#ifndef NOC_G8_FWD_DEPTH_SPLIT
-#define NOC_G8_FWD_DEPTH_SPLIT 2
-#endif
-// 1: a full solve is a backward launch + a forward-only launch (see kkt_group8_kernel's FWD)
-#ifndef NOC_G8_SPLIT
-#define NOC_G8_SPLIT 0
-#endif
+// stages of the forward sweep's loads in flight per wave (deeper rings spill)
+constexpr int kFwdDepth = 2;
 // Broadcast lane J of every 8-lane group to the whole group on the VALU (DPP row_newbcast: lane n
 // of each 16-lane row to the row; bank_mask 0x3 writes lanes 0-7 of the row from row lane J, 0xC
 // lanes 8-15 from row lane 8+J) instead of a ds_bpermute through the LDS pipe, which the backward
@@ -97,7 +85,6 @@ NOC_DEV double bcast8(double x) {
 }
 // group broadcast with a (post-unrolling) constant source lane
 NOC_DEV double gb(double x, int j) {
-#if NOC_G8_DPP
   switch (j) {
     case 0: return bcast8<0>(x);
     case 1: return bcast8<1>(x);
@@ -108,16 +95,10 @@ NOC_DEV double gb(double x, int j) {
     case 6: return bcast8<6>(x);
     default: return bcast8<7>(x);
   }
-#else
-  return gshfl(x, j, TPW);
-#endif
 }
 }  // namespace g8
 
-// FWD: the forward sweep alone, as its own launch after a MODE_BWD launch of the fused kernel
-// (launch_kkt_group8): its register budget is then its own, so its prefetch ring can be deeper
-// (NOC_G8_FWD_DEPTH_SPLIT stages instead of the fused kernel's NOC_G8_FWD_DEPTH, which the
-// backward sweep's 245 registers leave no room for).  K and d go through HBM either way.
+// FWD: the forward sweep alone (MODE_FWD: paroc.par_fwd_pass, the gains are inputs); no LDS.
 template <bool AFF, bool TILED, bool FWD = false>
 __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kernel(KKTArgs a) {
   using namespace g8;
@@ -330,7 +311,7 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
     __threadfence_block();  // this group's K, d stores are visible to its other lanes below
   }
 
-  // ---------------- forward rollout of the closed loop (NOC_G8_FWD_DEPTH stages in flight) ----
+  // ---------------- forward rollout of the closed loop (kFwdDepth stages in flight) ----
   const size_t tNc = (size_t)trajc * N;
   Vec<NX> x;
   set_zero(x);
@@ -352,7 +333,7 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       cv = (AFF && a.c) ? a.c[si * NX + q] : 0.0;
     }
   };
-  // Ring of NOC_G8_FWD_DEPTH stage buffers, the loop unrolled by the depth so every buffer has a
+  // Ring of kFwdDepth stage buffers, the loop unrolled by the depth so every buffer has a
   // fixed register home: stage s is computed from buffer s % DEPTH, which is then refilled with
   // stage s + DEPTH.  (A rotating k0 <- k1 copy reads the prefetch registers and makes the
   // compiler wait for the newest loads -- a vmcnt(0) per stage that left one stage of latency
@@ -377,7 +358,7 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
   // The refill loads are unconditional (stage index clamped to N - 1; the surplus reads are
   // never used): a data-dependent skip would leave the compiler unsure how many memory ops follow
   // a buffer's loads, and it then waits for all of them (vmcnt(0)) before every use.
-  constexpr int D = FWD ? NOC_G8_FWD_DEPTH_SPLIT : NOC_G8_FWD_DEPTH;
+  constexpr int D = kFwdDepth;
   auto clamp_s = [&](int t) { return t < N ? t : N - 1; };
   FwdStage fb[D];
   NOC_UNROLL for (int j = 0; j < D; ++j) load_fs(clamp_s(j), fb[j]);
@@ -415,17 +396,8 @@ static void launch_g8(const KKTArgs& a, unsigned grid, hipStream_t stream) {
 [[maybe_unused]] static hipError_t launch_kkt_group8(const KKTArgs& a, hipStream_t stream) {
   if (!a.K || !a.d) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.B + g8::TPW - 1) / g8::TPW);
-  if (a.mode == MODE_FWD) {
-    launch_g8<true>(a, grid, stream);
-  } else if (a.mode == MODE_BWD || !NOC_G8_SPLIT) {
-    launch_g8<false>(a, grid, stream);
-  } else {  // full solve: backward launch, then the forward-only launch (ablation bits 1 / 6 drop one)
-    KKTArgs ab = a, af = a;
-    ab.mode = MODE_BWD;
-    af.mode = MODE_FWD;
-    if (!(a.ablate & 64)) launch_g8<false>(ab, grid, stream);
-    if (!(a.ablate & 2)) launch_g8<true>(af, grid, stream);
-  }
+  if (a.mode == MODE_FWD) launch_g8<true>(a, grid, stream);
+  else launch_g8<false>(a, grid, stream);
   return hipGetLastError();
 }
 

@@ -975,7 +975,18 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     return;
   }
   if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) slot[N * KD + i] = x[i];
-  __syncthreads();  // orders the segment's LDS writes (one or two waves) before its reads
+  // order the segment's LDS writes before its reads.  One-wave segments: a wave-scope fence --
+  // a wave's LDS accesses complete in issue order, and the independent waves that share a
+  // workgroup (kkt_waves_per_block) neither wait for each other nor depend on ended waves
+  // leaving s_barrier.  Two-wave segments: the workgroup barrier (both waves of the block are
+  // the one trajectory, so they return together).
+  if constexpr (W > 1) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
   if (a.dx) {
     double* dst = a.dx + (tN + traj) * NX;
     if constexpr (NX % 2 == 0) {

@@ -469,6 +469,20 @@ int noc_lqr_params(int nx, int nu, int N, int B, const double* lam, const double
   return hip_status(noc::lqr_params(a, static_cast<hipStream_t>(stream)), "lqr_params");
 }
 
+int noc_check_feasibility(const noc_family* fam, int N, int B, const double* x, const double* u,
+                          int* feasible, void* stream) {
+  if (!fam) return fail(-2, "family is NULL");
+  if (!noc::family_supported(*fam)) return fail(-1, "unsupported problem family (kind/nx/nu)");
+  if (N < 1 || B < 0) return fail(-1, "need N >= 1, B >= 0");
+  int rc = 0;
+  if ((rc = check_ptr(x, "x", true, 8)) || (rc = check_ptr(u, "u", true, 8)) ||
+      (rc = check_ptr(feasible, "feasible", true, 4)))
+    return rc;
+  if (B == 0) return 0;
+  return hip_status(noc::traj_feasibility(*fam, N, B, x, u, feasible,
+                                          static_cast<hipStream_t>(stream)), "check_feasibility");
+}
+
 static int kkt_and_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* stream) {
   // the trial step needs dx, du only: gains stay on chip when they fit (ws->K, ws->d otherwise)
   const bool on_chip = noc_kkt_gains_on_chip(fam->nx, fam->nu, ws->N, ws->lanes) == 1;

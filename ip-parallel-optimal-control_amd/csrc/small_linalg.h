@@ -534,8 +534,13 @@ NOC_DEV void lu_pp_solve(double (&X)[N][N], double (&Y)[N][NR]) {
 }
 
 // Y <- X^{-1} Y for a 2 x 2 X in closed form: one division (the adjugate over det), no pivoting.
-// Used where det(X) is bounded away from 0 by construction (X = I + C J with C, J >= 0:
-// det = 1 + tr(CJ) + det(C) det(J) >= 1); Cramer's rule is forward stable for n = 2.
+// Used for the combine's X = I + C1 J2.  C1 (a controllability Gramian) is PSD, but the value
+// Hessian J2 is not in general: Q = cxx + lambda.fxx, or a traced user cost, can make it
+// indefinite, and then det(X) = 1 + tr(C1 J2) + det(C1) det(J2) can be small or zero.  Nothing is
+// checked here: an exactly singular X gives inf / NaN in the step (reported as data, never a
+// fault).  For n = 2 Cramer's rule is as accurate as elimination with partial pivoting, so a
+// nearly singular X costs no more accuracy than the pivoting path would (tests/test_kkt_gpu.py:
+// indefinite Q at nx = 2 against the oracle).
 template <int NR>
 NOC_DEV void solve2_closed(const double (&X)[2][2], double (&Y)[2][NR]) {
   const double det = X[0][0] * X[1][1] - X[0][1] * X[1][0];

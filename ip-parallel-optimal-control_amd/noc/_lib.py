@@ -100,6 +100,7 @@ SIGNATURES.update({
     "noc_final_cost_derivs": (_i, [_fp, _i, _dp, _dp, _dp, _dp]),
     "noc_costates": (_i, [_i, _i, _i, _dp, _dp, _dp, _dp, _i, _dp]),
     "noc_lqr_params": (_i, [_i] * 4 + [_dp] * 13 + [_dp]),
+    "noc_check_feasibility": (_i, [_fp, _i, _i, _dp, _dp, _dp, _dp]),
     "noc_ddp_work_doubles": (ctypes.c_longlong, [_i, _i, _i, _i]),
     "noc_ddp_supported": (_i, [_fp]),
     "noc_ddp_solve": (_i, [_fp, _i, _i] + [_dp] * 6 + [ctypes.c_double, _i, _dp]),

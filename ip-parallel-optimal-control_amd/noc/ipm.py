@@ -9,6 +9,7 @@ single "any trajectory not done" flag every `poll_every` iterations.
 """
 from __future__ import annotations
 
+import math
 import ctypes
 from typing import Optional
 
@@ -28,6 +29,18 @@ def persistent_supported(family, N: int) -> bool:
     """noc_ipm_solve_supported: the whole-solve kernel handles this family / horizon (lanes 64)."""
     lib = _lib.load_for(family)
     return lib.noc_ipm_solve_supported(ctypes.byref(family.to_c()), int(N), 64) == 1
+
+
+def carve_zeros(spec, device, dtype, align_bytes: int = 256):
+    """{name: shape} -> ({name: zero view}, backing tensor): one allocation, every field starting
+    on an align_bytes boundary."""
+    per = max(align_bytes // torch.empty((), dtype=dtype).element_size(), 1)
+    offs, n = {}, 0
+    for k, s in spec.items():
+        offs[k] = n
+        n += -(-math.prod(s) // per) * per
+    buf = torch.zeros(max(n, 1), device=device, dtype=dtype)
+    return {k: buf[offs[k]:offs[k] + math.prod(s)].view(s) for k, s in spec.items()}, buf
 
 
 class BatchedIPM:
@@ -67,11 +80,15 @@ class BatchedIPM:
                       M=tiled(nx * nu), r=tiled(nu), P=(Bt, nx, nx), cx=tiled(nx),
                       cu=tiled(nu), lc=tiled(1), lam=(Bt, N + 1, nx), dx=(Bt, N + 1, nx),
                       du=(Bt, N, nu), pred=(Bt,), K=tiled(nu * nx), d=tiled(nu))
-        self.t = {k: torch.zeros(s, **f64) for k, s in shapes.items()}
-        for k in _lib.WS_INT_FIELDS:
-            self.t[k] = torch.zeros(Bt, **i32)
         for k in _lib.WS_STATE_FIELDS:
-            self.t[k] = torch.zeros(Bt, **f64)
+            shapes[k] = (Bt,)
+        # one zero-filled allocation per dtype (two fill launches instead of one per field: the
+        # host cost of a B = 1 call)
+        self.t, self._bufs = {}, []
+        for spec, kw in ((shapes, f64), ({k: (Bt,) for k in _lib.WS_INT_FIELDS}, i32)):
+            views, buf = carve_zeros(spec, **kw)
+            self.t.update(views)
+            self._bufs.append(buf)
         ws = _lib.NocIpmWs()
         ws.Bt, ws.N, ws.lanes = Bt, N, L
         for k in _lib.WS_DOUBLE_FIELDS + _lib.WS_INT_FIELDS + _lib.WS_STATE_FIELDS:
@@ -188,8 +205,9 @@ class BatchedIPM:
         """Run the barrier schedule to completion for every trajectory.  Returns the KKT solves of
         the slowest trajectory (kkt_solves.max(), on both paths).  max_steps caps the KKT solves
         of every trajectory on both paths: the persistent solve stops a trajectory at that many
-        solves (resumable); the multi-launch loop stops once every trajectory is done or at or
-        past the cap (one launch may account up to 501 identical retries, P:151-188).
+        solves (resumable); the multi-launch loop stops once every trajectory that is still running
+        is at or past the cap (trajectories that finished earlier do not hold it back; one launch
+        may account up to 501 identical retries, P:151-188).
         terminal=None: the reference's choice for the mode (par: XT = Q[0], P:73; seq:
         hessian(final_cost), S:66)."""
         terminal = default_terminal(mode) if terminal is None else terminal
@@ -202,8 +220,10 @@ class BatchedIPM:
                 self.step(mode, terminal)
             if self.all_done():
                 break
-            if max_steps is not None and int(self.t["kkt_solves"].min().item()) >= max_steps:
-                break
+            if max_steps is not None:
+                running = self.t["phase"] != _lib.PHASE_DONE
+                if int(self.t["kkt_solves"][running].min().item()) >= max_steps:
+                    break
         return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
 
     def tiled_blocks(self):

@@ -91,15 +91,32 @@ def compute_lqr_params(lagrange_multipliers, d: Derivatives):
 
 
 def check_traj_feasibility(ocp: OCP, x, u):
-    """P:45-47: all(constraints(x_k, u_k) <= 0) -- for the registered families' box constraints
-    |u_j| <= u_bound (none when u_bound <= 0); one flag per trajectory if batched."""
+    """P:45-47: all(constraints(x_k, u_k) <= 0) over k < N (x[:-1] paired with u) with the
+    family's whole constraint vector -- the built-ins' box on u, a registered family's traced
+    constraints(x, u) including state constraints (noc_check_feasibility, one wave per
+    trajectory).  x (N+1, nx), u (N, nu) -> a 0-d bool tensor; batched (B, N+1, nx), (B, N, nu)
+    -> (B,) bool."""
     fam = _family(ocp)
-    u = _dev(u, "u")
-    if fam.u_bound <= 0:
-        ok = torch.ones(u.shape[:-2], dtype=torch.bool, device=u.device)
-    else:
-        ok = ((u - fam.u_bound <= 0) & (-u - fam.u_bound <= 0)).flatten(-2).all(-1)
-    return ok
+    x, u = _dev(x, "x"), _dev(u, "u")
+    single = u.dim() == 2
+    if single:
+        x, u = x[None], u[None]
+    if x.dim() != 3 or u.dim() != 3 or x.shape[0] != u.shape[0] or x.shape[1] != u.shape[1] + 1 \
+            or x.shape[2] != fam.nx or u.shape[2] != fam.nu:
+        raise _lib.NocError(f"check_traj_feasibility: need x (B, N+1, {fam.nx}) and u (B, N, "
+                            f"{fam.nu}); got {tuple(x.shape)} and {tuple(u.shape)}")
+    B, N = u.shape[0], u.shape[1]
+    if N == 0:  # jnp.all of an empty constraint array
+        ok = torch.ones(B, dtype=torch.bool, device=u.device)
+        return ok[0] if single else ok
+    ok = torch.empty(B, dtype=torch.int32, device=u.device)
+    lib = _lib.load_for(fam)
+    _lib.check(lib.noc_check_feasibility(ctypes.byref(fam.to_c()), N, B, x.data_ptr(),
+                                         u.data_ptr(), ok.data_ptr(),
+                                         _lib.stream_handle(u.device)),
+               "noc_check_feasibility", lib)
+    ok = ok.bool()
+    return ok[0] if single else ok
 
 
 def noc_to_lqt(ru, Q, R, M, A, B):
@@ -156,9 +173,9 @@ def _run(ocp: OCP, controls, initial_state, mode, terminal="stage0", lanes=0,
     eng.load(u, x0)
     bp0 = 0.1 if one_stage_bp is None else float(one_stage_bp)
     steps = eng.solve(mode=mode, terminal=_TERMINAL[terminal], bp0=bp0)
-    U, iters, solves = eng.result()
-    X = eng.t["x"].cpu().numpy()
-    U, iters, solves = U.cpu().numpy(), iters.cpu().numpy(), solves.cpu().numpy()
+    t = eng.t  # straight to the host (result() would clone on the device first)
+    U, iters, solves = t["u"].cpu().numpy(), t["total_it"].cpu().numpy(), t["kkt_solves"].cpu().numpy()
+    X = t["x"].cpu().numpy()
     if single:
         U, iters, solves, X = U[0], int(iters[0]), int(solves[0]), X[0]
     if one_stage_bp is not None:

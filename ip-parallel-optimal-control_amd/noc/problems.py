@@ -189,16 +189,33 @@ def make_problem(name: str, N: int) -> OCP:
     raise ValueError(name)
 
 
+def shard_initial_conditions(name: str, N: int, global_batch: int, lo: int, hi: int,
+                             seed: int = 0):
+    """Trajectories lo..hi-1 of ONE global batch (initial_conditions(name, N, global_batch,
+    seed)): every rank of a sharded run draws the same global problem and keeps its slice, so the
+    shards of N ranks concatenate to exactly the 1-rank inputs."""
+    if not 0 <= lo <= hi <= global_batch:
+        raise ValueError(f"shard [{lo}, {hi}) outside the global batch {global_batch}")
+    x0, u0 = initial_conditions(name, N, global_batch, seed)
+    return x0[lo:hi].copy(), u0[lo:hi].copy()
+
+
 def make_bench_blocks(name: str, N: int, batch: int, seed: int = 0, device="cuda", lanes: int = 0,
-                      natural: bool = False):
+                      natural: bool = False, shard=None):
     """Realistic LQ blocks of the first Newton step (bp = 0.1, rp = 1) of `batch` trajectories,
     produced on the GPU by the HIP linearisation kernels, in the KKT scan's tiled layout
     (`tiled`: noc.lqt.TiledBlocks).  natural=True also returns the natural-layout copies
-    (A, B, Q, R, M, r, P) for checks.  `reg`, `x`, `u` are natural."""
+    (A, B, Q, R, M, r, P) for checks.  `reg`, `x`, `u` are natural.  shard = (global_batch, lo):
+    the trajectories lo..lo+batch-1 of one global batch (shard_initial_conditions) instead of a
+    batch of its own."""
     from .ipm import BatchedIPM
     from .lqt import pick_lanes
     ocp = make_problem(name, N)
-    x0, u0 = initial_conditions(name, N, batch, seed)
+    if shard is None:
+        x0, u0 = initial_conditions(name, N, batch, seed)
+    else:
+        G, lo = shard
+        x0, u0 = shard_initial_conditions(name, N, G, lo, lo + batch, seed)
     # one all-active KKT launch over the batch: the batch-aware lanes policy
     lanes = lanes or pick_lanes(ocp.family.nx, ocp.family.nu, N, batch)
     # the interior-point workspace's tiled layout spans one wave (lanes <= 64); two-wave segments

@@ -48,3 +48,45 @@ def test_bench_gpus_1_is_one_process():
     assert p.returncode == 0, p.stderr[-2000:]
     (line,) = _lines(p.stdout)
     assert line["n_gpus"] == 1 and line["ranks_seen"] == [0]
+
+
+def _dump(tmp_path, gpus, extra=()):
+    d = tmp_path / f"w{gpus}"
+    d.mkdir()
+    p = subprocess.run([sys.executable, BENCH, "--gpus", str(gpus), "--steps", "1",
+                        "--global-batch", "37", "--horizon", "20", *extra],
+                       env=_env(NOC_BENCH_DRYRUN_DUMP=str(d)), capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    import numpy as np
+    parts = [np.load(d / f"rank{r}_of{gpus}.npz") for r in range(gpus)]
+    return parts, _lines(p.stdout)[0]
+
+
+def test_bench_shards_one_global_batch(tmp_path):
+    """every rank of the strong-scaling bench draws the SAME global batch
+    (one seed) and keeps its shard_bounds slice, so the N-rank shards concatenate to exactly the
+    1-rank inputs (bit for bit) -- the N-rank line solves the 1-rank problem."""
+    import numpy as np
+    (one,), line1 = _dump(tmp_path, 1)
+    assert line1["config"]["global_batch"] == 37 and line1["scaling"] == "strong"
+    for gpus in (2, 4):
+        parts, line = _dump(tmp_path, gpus)
+        assert line["config"]["global_batch"] == 37
+        los = [int(q["lo"]) for q in parts]
+        assert los == sorted(los) and los[0] == 0
+        for k in ("x0", "u0"):
+            cat = np.concatenate([q[k] for q in parts])
+            assert np.array_equal(cat, one[k]), (gpus, k)
+
+
+def test_bench_weak_scaling_slices(tmp_path):
+    """--batch B (weak scaling): rank r owns trajectories [rB, (r+1)B) of the global B x world."""
+    import numpy as np
+    parts, line = _dump(tmp_path, 2, ("--batch", "5"))
+    assert line["scaling"] == "weak" and line["config"]["global_batch"] == 10
+    sys.path.insert(0, os.path.join(ROOT, "ip-parallel-optimal-control_amd"))
+    from noc import problems
+    x0, u0 = problems.initial_conditions("cartpole", 20, 10, seed=1234)
+    assert np.array_equal(np.concatenate([q["x0"] for q in parts]), x0)
+    assert np.array_equal(np.concatenate([q["u0"] for q in parts]), u0)

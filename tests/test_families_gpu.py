@@ -214,3 +214,66 @@ def test_traced_cost_family_rejects_ddp_and_mixed_costs():
         families.register_family("bad", CF.cartpole_ode, 4, 1, dt=0.02, wx=[1.0] * 4,
                                  stage_cost=CF.track_limit_stage_cost,
                                  final_cost=CF.track_limit_final_cost, build=False)
+
+
+def _host_feasible(ocp, X, U):
+    """P:45-47 evaluated with the OCP's own host callables: all(constraints(x_k, u_k) <= 0), k < N."""
+    return bool(all(np.all(np.asarray(ocp.constraints(X[k], U[k])) <= 0) for k in range(len(U))))
+
+
+def test_check_traj_feasibility_state_constraint():
+    """check_traj_feasibility / check_feasibility (P:45-47, S:93-95) evaluate the family's whole
+    constraint vector on the device (noc_check_feasibility): a state beyond X_LIMIT is infeasible,
+    the solver's own states are feasible -- batched and unbatched, equal to the OCP's host
+    callables; a u beyond the box and a NaN state are infeasible; x_N is not tested (x[:-1])."""
+    from noc.ipm import BatchedIPM
+    from noc.par_interior_point_newton import check_traj_feasibility
+    from noc.seq_interior_point_newton import check_feasibility
+    import custom_families as CF
+    N, B = 50, 4
+    ocp = CF.cartpole_track_limit(1.0 / N)
+    x0, u0 = _tl_inputs(N, B, 3)
+    eng = BatchedIPM(ocp.family, N, B, lanes=64, persistent=True)
+    eng.load(u0, x0)
+    eng.solve()
+    torch.cuda.synchronize()
+    U, X = eng.result()[0].cpu().numpy(), eng.t["x"].cpu().numpy()
+    cases = [X.copy() for _ in range(4)]
+    cases[1][1, 17, 0] = CF.X_LIMIT + 1e-3       # cart beyond the track limit
+    cases[2][2, 0, 0] = -(CF.X_LIMIT + 0.25)     # at stage 0
+    cases[3][3, 9, 2] = np.nan                   # NaN compares false
+    Uc = [U.copy() for _ in range(4)]
+    Uc[0][0, N - 1, 0] = 50.5                    # the u box, last stage
+    tail = X.copy()
+    tail[:, N, 0] = 10.0                         # x_N is outside x[:-1]: still feasible
+    for Xc, Ucase in list(zip(cases, Uc)) + [(tail, U)]:
+        want = np.array([_host_feasible(ocp, Xc[b], Ucase[b]) for b in range(B)])
+        for fn in (check_traj_feasibility, check_feasibility):
+            got = fn(ocp, Xc, Ucase).cpu().numpy()
+            assert got.dtype == np.bool_ and np.array_equal(got, want), (got, want)
+            for b in range(B):
+                one = fn(ocp, Xc[b], Ucase[b])
+                assert one.dim() == 0 and bool(one) == want[b]
+    assert np.all(np.array([_host_feasible(ocp, X[b], U[b]) for b in range(B)]))
+    assert not _host_feasible(ocp, cases[1][1], U[1])
+
+
+def test_check_traj_feasibility_builtin_box():
+    """The built-ins' constraint is the u box (|u| <= u_bound): the device verdict equals the host
+    callables' at random feasible / infeasible controls, for the pendulum and cart-pole."""
+    from noc import problems
+    from noc.par_interior_point_newton import check_traj_feasibility
+    rng = np.random.default_rng(7)
+    for name, ocp, N in (("pendulum", problems.pendulum(0.01), 100),
+                         ("cartpole", problems.cartpole(0.005), 200)):
+        B = 70
+        x0, u = problems.initial_conditions(name, N, B, seed=4)
+        X = rng.normal(size=(B, N + 1, ocp.family.nx))
+        ub = ocp.family.u_bound
+        u = np.clip(u, -0.9 * ub, 0.9 * ub)
+        hit = rng.integers(0, N, size=B)
+        for b in range(0, B, 3):
+            u[b, hit[b], 0] = (1 if b % 2 else -1) * ub * 1.0001
+        want = np.array([_host_feasible(ocp, X[b], u[b]) for b in range(B)])
+        assert 0 < want.sum() < B
+        assert np.array_equal(check_traj_feasibility(ocp, X, u).cpu().numpy(), want)

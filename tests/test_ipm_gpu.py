@@ -246,6 +246,34 @@ def test_persistent_solve_respects_solve_cap(wide, monkeypatch):
     assert np.all(eng.t["phase"].cpu().numpy() != _lib.PHASE_DONE)
 
 
+def test_multilaunch_max_steps_caps_running_trajectories():
+    """The multi-launch loop's max_steps: trajectories that finished below the cap do not hold
+    the loop open (the cap is tested on the still-running ones), so a capped solve stops with
+    slow trajectories unfinished at or past the cap while the fast ones are done with exactly
+    their uncapped results."""
+    from noc import problems, _lib
+    from noc.ipm import BatchedIPM
+    N, Bt = 50, 16
+    ocp = problems.pendulum(1.0 / N)
+    x0, u0 = problems.initial_conditions("pendulum", N, Bt, seed=4)
+    eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=False)
+    eng.load(u0, x0)
+    eng.solve()
+    torch.cuda.synchronize()
+    U_full, _, s_full = (t.cpu().numpy() for t in eng.result())
+    cap = int(s_full.min()) + 1
+    assert int(s_full.max()) > cap + 8 * 2  # the batch spreads (seeded)
+    eng.load(u0, x0)
+    eng.solve(max_steps=cap)
+    torch.cuda.synchronize()
+    U, _, s = (t.cpu().numpy() for t in eng.result())
+    phase = eng.t["phase"].cpu().numpy()
+    done, running = phase == _lib.PHASE_DONE, phase != _lib.PHASE_DONE
+    assert done.any() and running.any()
+    assert np.all(s[running] >= cap)
+    assert np.array_equal(s[done], s_full[done]) and np.array_equal(U[done], U_full[done])
+
+
 @pytest.mark.parametrize("name,N,Bt,mode", [
     ("pendulum", 60, 16, "par"), ("pendulum", 60, 16, "seq"),
     ("pendulum", 20, 4, "par"),      # N < 64: most lanes of every wave own no stage
