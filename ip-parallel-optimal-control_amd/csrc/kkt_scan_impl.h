@@ -975,18 +975,12 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     return;
   }
   if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) slot[N * KD + i] = x[i];
-  // order the segment's LDS writes before its reads.  One-wave segments: a wave-scope fence --
-  // a wave's LDS accesses complete in issue order, and the independent waves that share a
-  // workgroup (kkt_waves_per_block) neither wait for each other nor depend on ended waves
-  // leaving s_barrier.  Two-wave segments: the workgroup barrier (both waves of the block are
-  // the one trajectory, so they return together).
-  if constexpr (W > 1) {
-    __syncthreads();
-  } else {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
+  // orders the segment's LDS writes (one or two waves) before its reads.  With several
+  // independent waves per workgroup (kkt_waves_per_block) every wave of the block reaches this one
+  // barrier: the scan kernel sends waves without a trajectory to it too (kkt_scan_kernel).  (A
+  // wave-scope fence instead -- no cross-wave wait -- measured 0.5-1.5 % slower at c3 and the
+  // 512 shard, profiles/r04/fence_ab/.)
+  __syncthreads();
   if (a.dx) {
     double* dst = a.dx + (tN + traj) * NX;
     if constexpr (NX % 2 == 0) {
@@ -1035,7 +1029,18 @@ __global__ __launch_bounds__(L > 64 ? L : 256, L > 64 ? 1 : NOC_KKT_WAVES_PER_SI
   // SIMDs; the launch policy (kkt_pick_lanes) uses L = 128 only when every wave is then resident
   // at once (B * 2 <= #SIMDs).
   if constexpr (L > 64) asm volatile("" ::: "a255");
-  kkt_scan_wave<NX, NU, L, AFF, TILED, CACHE>(a, tid / L, tid % L);
+  const int traj = tid / L;
+  if constexpr (L <= 64) {
+    // a wave with no trajectory to solve (past the batch, or masked off) still meets the one
+    // workgroup barrier its block's other waves reach at the copy-out (lds_out, full / forward
+    // mode), so no wave of the block waits on a wave that has ended.  Uniform over the segment;
+    // two-wave segments (L = 128) are one trajectory per block, so their blocks return together.
+    if (traj >= a.B || (a.active && a.active[traj] == 0)) {
+      if (a.lds_out && a.mode != MODE_BWD) __syncthreads();
+      return;
+    }
+  }
+  kkt_scan_wave<NX, NU, L, AFF, TILED, CACHE>(a, traj, tid % L);
 }
 
 // Register-cached chunk length for (NX, NU, L): only where a short chunk's blocks fit beside the

@@ -243,5 +243,20 @@ class BatchedIPM:
                     P=t["P"])
 
     # -------------------------------------------------------------------------------------------
+    def host_result(self):
+        """(u, total_it, kkt_solves, x) as numpy arrays in two device-to-host copies: x and u are
+        neighbours in the fp64 workspace allocation, total_it and kkt_solves in the int32 one, so
+        each pair leaves as one contiguous span (the per-call host cost of small solves)."""
+        out = {}
+        for buf, names in ((self._bufs[0], ("x", "u")), (self._bufs[1], ("total_it", "kkt_solves"))):
+            es = buf.element_size()
+            offs = {k: (self.t[k].data_ptr() - buf.data_ptr()) // es for k in names}
+            lo = min(offs.values())
+            hi = max(offs[k] + self.t[k].numel() for k in names)
+            host = buf[lo:hi].cpu().numpy()
+            for k in names:
+                out[k] = host[offs[k] - lo:offs[k] - lo + self.t[k].numel()].reshape(self.t[k].shape)
+        return out["u"], out["total_it"], out["kkt_solves"], out["x"]
+
     def result(self):
         return (self.t["u"].clone(), self.t["total_it"].clone(), self.t["kkt_solves"].clone())

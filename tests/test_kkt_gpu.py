@@ -376,3 +376,25 @@ def test_mpc_loop_matches_oracle_closed_loop(graph, batched):
             assert np.max(np.abs(got_u - du[0])) <= 1e-9 * max(1.0, np.abs(du[0]).max()), t
             assert np.max(np.abs(got_x - dx[1])) <= 1e-10 * max(1.0, np.abs(dx[1]).max()), t
             x = dx[1]
+
+
+@pytest.mark.parametrize("lanes", [64, 128, 16])
+def test_nx2_indefinite_state_cost(lanes):
+    """nx = 2 combines use the closed-form 2 x 2 solve (small_linalg.h: solve2_closed) with no
+    pivoting or threshold check.  With an indefinite state cost Q (as cxx + lambda.fxx, or a traced
+    user cost, can be) the value Hessians are indefinite and det(I + C1 J2) is no longer >= 1;
+    the step must still match the oracle at 1e-10 wherever the KKT system is well posed
+    (all Quu > 0), and the feasibility flags must agree."""
+    case = rand_lq(77 + lanes, 6, 60, 2, 1)
+    case["Q"] = case["Q"] - 0.6 * np.eye(2)     # eigenvalues of H's state block start at 0.1
+    case["R"] = case["R"] + 2.0
+    ref = oracle_batch(case)
+    out = run_kkt(case, lanes)
+    assert np.array_equal(out["feasible"].astype(bool), ref["feasible"].astype(bool))
+    ok = np.flatnonzero(ref["feasible"].astype(bool))
+    assert ok.size >= 3, ref["feasible"]
+    J = case["Q"]
+    assert np.any(np.linalg.eigvalsh(J).min(axis=-1) < 0)  # the stage costs really are indefinite
+    for k in ("dx", "du", "K", "d", "S", "v"):
+        assert relerr(out[k][ok], ref[k][ok]) < RTOL, (k, relerr(out[k][ok], ref[k][ok]))
+    assert relerr(out["pred"][ok], ref["pred"][ok]) < RTOL
