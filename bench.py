@@ -153,7 +153,7 @@ def ipm_solve_rate(problem, N, B, rank, world, G, lo, seed=11):
         eng.load(u0, x0)
         eng.ws.flags = flags
         torch.cuda.synchronize()
-        if world > 1:
+        if pg():
             dist.barrier()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
@@ -176,7 +176,7 @@ def ipm_solve_rate(problem, N, B, rank, world, G, lo, seed=11):
     tot = [float(solves.sum()), float(done), float(its.double().sum()), float(B),
            float(reps.sum()), float(not identical)]
     mx = [ms, float(solves.max()), ms_all, ms_index]
-    if world > 1:
+    if pg():
         tot = allreduce(tot, "sum")
         mx = allreduce(mx, "max")
     computed = tot[0] - tot[4]
@@ -197,6 +197,13 @@ def ipm_solve_rate(problem, N, B, rank, world, G, lo, seed=11):
 
 
 BENCH_SEED = 1234  # the global batch's seed (the same on every rank)
+
+
+def pg():
+    """True when this run has a process group (launched ranks): barriers and max / sum / gather
+    over the ranks go through it."""
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
 
 
 def rank_shard(args, world, rank):
@@ -242,10 +249,10 @@ def dry_run_line(args, world, rank):
     if dump:  # this rank's inputs, for the CPU test that they are a slice of the 1-rank inputs
         import numpy as np
         np.savez(os.path.join(dump, f"rank{rank}_of{world}.npz"), x0=x0, u0=u0, lo=lo, G=G)
-    if world > 1:
+    if pg():
         dist.barrier()
     t = [0.0]
-    if world > 1:
+    if pg():
         t = allreduce(t, "max")
         ranks = allgather_float(float(rank))
     else:
@@ -315,7 +322,9 @@ def main():
         local = 0
     if not dry:
         torch.cuda.set_device(local)
-    if world > 1:
+    # a process group whenever a launcher started this process (world 1 included: the RCCL
+    # init / barrier / all-reduce / all-gather then run on the hardware even on one GPU)
+    if world > 1 or "WORLD_SIZE" in os.environ:
         if rehearsal or dry:
             dist.init_process_group("gloo")
         else:
@@ -324,7 +333,7 @@ def main():
         line = dry_run_line(args, world, rank)
         if rank == 0:
             print(json.dumps(line), flush=True)
-        if world > 1:
+        if pg():
             dist.destroy_process_group()
         return
     from noc import lqt, problems, _lib
@@ -374,7 +383,7 @@ def main():
         else:
             step()
     torch.cuda.synchronize()
-    if world > 1:
+    if pg():
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -388,19 +397,19 @@ def main():
     ev1.record()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    if world > 1:
+    if pg():
         dist.barrier()
     torch.cuda.synchronize()
     kern_ms = ev0.elapsed_time(ev1) / args.steps          # HIP-event time per launch (stream)
     ms = wall * 1e3 / args.steps
     rank_kern_ms = [kern_ms]
-    if world > 1:
+    if pg():
         rank_kern_ms = allgather_float(kern_ms)
         ms, kern_ms = allreduce([ms, kern_ms], "max")
     feasible_frac = float(out.feasible.float().mean())
     value = G * args.steps / (ms * args.steps / 1e3)
     abytes = algorithmic_bytes(nx, nu, N, B)
-    if world > 1:  # the slowest rank's bytes (shards differ by at most one trajectory)
+    if pg():  # the slowest rank's bytes (shards differ by at most one trajectory)
         abytes = int(allreduce([abytes], "max")[0])
     achieved = abytes / (kern_ms * 1e-3) / 1e9
     traffic, traffic_note = pmc_traffic(args.pmc_json, f"{args.problem}_N{N}_B{B}")
@@ -442,8 +451,8 @@ def main():
                      "traffic_note": traffic_note,
                      "algorithmic_bytes_per_launch": abytes, "kernel_ms": kern_ms,
                      "limiter": limiter},
-        "rccl_world_size": dist.get_world_size() if world > 1 else 1,
-        "process_group": (dist.get_backend() if world > 1 else None),
+        "rccl_world_size": dist.get_world_size() if pg() else 1,
+        "process_group": (dist.get_backend() if pg() else None),
         "per_rank_kernel_ms": rank_kern_ms,
         "feasible_fraction": feasible_frac,
         "launch": "eager" if graph is None else "hip_graph (the K timed steps captured once, one replay)",
@@ -460,7 +469,7 @@ def main():
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if pg():
         dist.destroy_process_group()
 
 

@@ -17,8 +17,12 @@ def main():
     import torch
     import torch.distributed as dist
     name, N, B, persistent = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4] == "1"
-    dist.init_process_group("gloo")
     torch.cuda.set_device(0)
+    backend = os.environ.get("NOC_DIST_BACKEND", "gloo")  # nccl (= RCCL): world 1 on one GPU
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo")
     from noc import problems, distributed as D
     from noc.ipm import BatchedIPM
     ocp = problems.make_problem(name, N)
@@ -35,7 +39,8 @@ def main():
         assert np.array_equal(its, itr) and np.array_equal(solves, sr)
         assert info["not_done"] == 0
         assert info["convergence_norm"] == float(eng.t["hu"].max().item())
-        print(f"SHARD_OK {name} N={N} B={B} persistent={persistent} world={dist.get_world_size()}",
+        print(f"SHARD_OK {name} N={N} B={B} persistent={persistent} world={dist.get_world_size()} "
+              f"backend={dist.get_backend()}",
               flush=True)
     dist.barrier()
     dist.destroy_process_group()
