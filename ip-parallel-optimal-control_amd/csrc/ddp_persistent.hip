@@ -46,11 +46,13 @@ struct DdpArgs {
   int *iterations, *passes, *done;
 };
 
-// per-stage derivative record: fx | fu | cx | cu | cuu (diagonal) | Hxx_i | Hxu_i | Huu_i (i < nx)
+// per-stage derivative record: fx | fu | cx | cu | cxx | cuu | cxu (the stage cost's full Hessian,
+// D:43-45 -- a registered family's traced cost is not diagonal) | Hxx_i | Hxu_i | Huu_i (i < nx)
 template <int NX, int NU>
 struct Rec {
-  static constexpr int FX = 0, FU = FX + NX * NX, CX = FU + NX * NU, CU = CX + NX, CUU = CU + NU,
-                       HXX = CUU + NU, HXU = HXX + NX * NX * NX, HUU = HXU + NX * NX * NU,
+  static constexpr int FX = 0, FU = FX + NX * NX, CX = FU + NX * NU, CU = CX + NX, CXX = CU + NU,
+                       CUU = CXX + NX * NX, CXU = CUU + NU * NU, HXX = CXU + NX * NU,
+                       HXU = HXX + NX * NX * NX, HUU = HXU + NX * NX * NU,
                        SIZE = HUU + NX * NU * NU;
 };
 
@@ -126,8 +128,15 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
         NOC_UNROLL for (int i = 0; i < NX; ++i) r[R::CX + i] = cx[i];
         NOC_UNROLL for (int j = 0; j < NU; ++j) {
           r[R::CU + j] = cu[j];
-          r[R::CUU + j] = f.stage_cuu(u, bp, j);
           g2 += cu[j] * cu[j];
+        }
+        {  // cxx, cuu, cxu (ipm_family.h: stage_hess; diag(wx), diag(wu + barrier), 0 for the
+           // parametrised cost, the generated Hessian of a traced one)
+          double cxx[NX * NX], cuu[NU * NU], cxu[NX * NU];
+          f.stage_hess(x, u, bp, cxx, cuu, cxu);
+          NOC_UNROLL for (int i = 0; i < NX * NX; ++i) r[R::CXX + i] = cxx[i];
+          NOC_UNROLL for (int i = 0; i < NU * NU; ++i) r[R::CUU + i] = cuu[i];
+          NOC_UNROLL for (int i = 0; i < NX * NU; ++i) r[R::CXU + i] = cxu[i];
         }
         if constexpr (KIND != NOC_FAMILY_LINEAR) {  // d2 f_i = add_hess_l with l = e_i
           NOC_UNROLL for (int i = 0; i < NX; ++i) {
@@ -165,11 +174,11 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
           double fx[NX * NX], fu[NX * NU];
           NOC_UNROLL for (int i = 0; i < NX * NX; ++i) fx[i] = r[R::FX + i];
           NOC_UNROLL for (int i = 0; i < NX * NU; ++i) fu[i] = r[R::FU + i];
-          // cxx = diag(wx), cxu = 0, cuu (stage cost); + Vx . d2f (D:43-45)
+          // cxx, cxu, cuu (the stage cost's Hessian); + Vx . d2f (D:43-45)
           double Qxx[NX * NX], Quu[NU * NU], Qxu[NX * NU];
-          NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) Qxx[i * NX + j] = (i == j) ? prm.wx[i] : 0.0;
-          NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int j = 0; j < NU; ++j) Quu[i * NU + j] = (i == j) ? r[R::CUU + i] : 0.0;
-          NOC_UNROLL for (int i = 0; i < NX * NU; ++i) Qxu[i] = 0.0;
+          NOC_UNROLL for (int i = 0; i < NX * NX; ++i) Qxx[i] = r[R::CXX + i];
+          NOC_UNROLL for (int i = 0; i < NU * NU; ++i) Quu[i] = r[R::CUU + i];
+          NOC_UNROLL for (int i = 0; i < NX * NU; ++i) Qxu[i] = r[R::CXU + i];
           if constexpr (KIND != NOC_FAMILY_LINEAR) {
             NOC_UNROLL for (int i = 0; i < NX; ++i) {
               NOC_UNROLL for (int m = 0; m < NX * NX; ++m) Qxx[m] += Vx[i] * r[R::HXX + i * NX * NX + m];
@@ -341,16 +350,14 @@ static hipError_t ddp_family(const noc_family& p, const DdpArgs& a, hipStream_t 
 }
 
 bool ddp_supported(const noc_family& p) {
-#ifdef NOC_CUSTOM_FAMILY
-  // a registered family with its own traced cost: the DDP record keeps the parametrised cost's
-  // diagonal Hessians only (the interior-point Newton solvers take any cost)
-  if (p.kind == NOC_FAMILY_CUSTOM && gen::kCustomCost) return false;
-#endif
-  return family_supported(p) && p.nx <= 4;  // one wave holds the nx x nx value Hessian
+  // any registered family's cost (parametrised or traced: the record holds the full Hessian);
+  // nx <= 4: every lane holds the value Hessian and the stage's Q blocks in registers
+  return family_supported(p) && p.nx <= 4;
 }
 
 long long ddp_record_doubles(int nx, int nu) {
-  return (long long)nx * nx + nx * nu + nx + 2 * nu + (long long)nx * (nx * nx + nx * nu + nu * nu);
+  return (long long)nx * nx + nx * nu + nx + nu + (long long)nx * nx + nu * nu + nx * nu +
+         (long long)nx * (nx * nx + nx * nu + nu * nu);
 }
 
 hipError_t ddp_solve(const noc_family& p, int N, int Bt, const double* x0, double* u,

@@ -199,14 +199,41 @@ def test_traced_cost_state_constraint_active_and_respected():
     assert np.all(xc <= CF.X_LIMIT) and np.all(xc.max(axis=1) > 0.9 * CF.X_LIMIT)
 
 
-def test_traced_cost_family_rejects_ddp_and_mixed_costs():
+def test_traced_cost_family_ddp_matches_oracle():
+    """Interior-point DDP (D:28-208) on the traced-cost, state-constrained cart-pole: the DDP
+    record carries the stage cost's full Hessian (cxx, cuu, cxu, D:43-45) from the generated
+    code, so a registered family's own cost runs through DDP too.  Against the oracle DDP on the
+    torch restatement (torch.func derivatives): as tests/test_ddp.py -- iterations and backward
+    passes within one, controls 1e-5, cost 1e-9 relative; the state constraint holds."""
+    from noc.differential_dynamic_programming import interior_point_ddp
+    from oracle import noc_oracle as O
+    import custom_families as CF
+    N, B = 30, 2
+    ocp = CF.cartpole_track_limit(1.0 / N)
+    x0, u0 = _tl_inputs(N, B, 5)
+    U, its, info = interior_point_ddp(ocp, u0, x0, return_info=True)
+    assert info["done"].all()
+    prob = O.NumpyProblem(CF.cartpole_track_limit_torch(1.0 / N))
+    for b in range(B):
+        Ur, itr, pr = O.interior_point_ddp(prob, u0[b], x0[b])
+        assert abs(int(its[b]) - itr) <= 1, (b, int(its[b]), itr)
+        assert abs(int(info["passes"][b]) - pr) <= 1, (b, int(info["passes"][b]), pr)
+        assert np.max(np.abs(U[b] - Ur)) < 1e-5, b
+        X = O.rollout(prob.dynamics, U[b], x0[b])
+        c = prob.total_cost(X, U[b], 0.8e-4)
+        cr = prob.total_cost(O.rollout(prob.dynamics, Ur, x0[b]), Ur, 0.8e-4)
+        assert abs(c - cr) <= 1e-9 * max(1.0, abs(cr)), b
+        assert np.all(np.abs(X[:-1, 0]) <= CF.X_LIMIT)
+
+
+def test_traced_cost_family_supports_ddp_and_rejects_mixed_costs():
     from noc import _lib
     from noc import families
     import custom_families as CF
     ocp = CF.cartpole_track_limit(1.0 / 50)
     lib = _lib.load_for(ocp.family)
     import ctypes
-    assert lib.noc_ddp_supported(ctypes.byref(ocp.family.to_c())) == 0
+    assert lib.noc_ddp_supported(ctypes.byref(ocp.family.to_c())) == 1
     with pytest.raises(_lib.NocError):
         families.register_family("bad", CF.cartpole_ode, 4, 1, dt=0.02,
                                  stage_cost=CF.track_limit_stage_cost, build=False)
