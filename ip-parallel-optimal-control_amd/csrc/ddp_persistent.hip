@@ -130,13 +130,14 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
           r[R::CU + j] = cu[j];
           g2 += cu[j] * cu[j];
         }
-        {  // cxx, cuu, cxu (ipm_family.h: stage_hess; diag(wx), diag(wu + barrier), 0 for the
-           // parametrised cost, the generated Hessian of a traced one)
+        if constexpr (Fam<KIND, NX, NU>::kGenCost) {  // cxx, cuu, cxu of a traced cost
           double cxx[NX * NX], cuu[NU * NU], cxu[NX * NU];
           f.stage_hess(x, u, bp, cxx, cuu, cxu);
           NOC_UNROLL for (int i = 0; i < NX * NX; ++i) r[R::CXX + i] = cxx[i];
           NOC_UNROLL for (int i = 0; i < NU * NU; ++i) r[R::CUU + i] = cuu[i];
           NOC_UNROLL for (int i = 0; i < NX * NU; ++i) r[R::CXU + i] = cxu[i];
+        } else {  // the parametrised cost: only the cuu diagonal varies along the trajectory
+          NOC_UNROLL for (int j = 0; j < NU; ++j) r[R::CUU + j * NU + j] = f.stage_cuu(u, bp, j);
         }
         if constexpr (KIND != NOC_FAMILY_LINEAR) {  // d2 f_i = add_hess_l with l = e_i
           NOC_UNROLL for (int i = 0; i < NX; ++i) {
@@ -174,11 +175,19 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
           double fx[NX * NX], fu[NX * NU];
           NOC_UNROLL for (int i = 0; i < NX * NX; ++i) fx[i] = r[R::FX + i];
           NOC_UNROLL for (int i = 0; i < NX * NU; ++i) fu[i] = r[R::FU + i];
-          // cxx, cxu, cuu (the stage cost's Hessian); + Vx . d2f (D:43-45)
+          // cxx, cxu, cuu (the stage cost's Hessian); + Vx . d2f (D:43-45).  The parametrised cost's
+          // Hessian is diag(wx), 0, diag(cuu): formed from the descriptor and the cuu diagonal
+          // (the same values as the record's, without loading them on this sequential path)
           double Qxx[NX * NX], Quu[NU * NU], Qxu[NX * NU];
-          NOC_UNROLL for (int i = 0; i < NX * NX; ++i) Qxx[i] = r[R::CXX + i];
-          NOC_UNROLL for (int i = 0; i < NU * NU; ++i) Quu[i] = r[R::CUU + i];
-          NOC_UNROLL for (int i = 0; i < NX * NU; ++i) Qxu[i] = r[R::CXU + i];
+          if constexpr (Fam<KIND, NX, NU>::kGenCost) {
+            NOC_UNROLL for (int i = 0; i < NX * NX; ++i) Qxx[i] = r[R::CXX + i];
+            NOC_UNROLL for (int i = 0; i < NU * NU; ++i) Quu[i] = r[R::CUU + i];
+            NOC_UNROLL for (int i = 0; i < NX * NU; ++i) Qxu[i] = r[R::CXU + i];
+          } else {
+            NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) Qxx[i * NX + j] = (i == j) ? prm.wx[i] : 0.0;
+            NOC_UNROLL for (int i = 0; i < NU; ++i) NOC_UNROLL for (int j = 0; j < NU; ++j) Quu[i * NU + j] = (i == j) ? r[R::CUU + i * NU + i] : 0.0;
+            NOC_UNROLL for (int i = 0; i < NX * NU; ++i) Qxu[i] = 0.0;
+          }
           if constexpr (KIND != NOC_FAMILY_LINEAR) {
             NOC_UNROLL for (int i = 0; i < NX; ++i) {
               NOC_UNROLL for (int m = 0; m < NX * NX; ++m) Qxx[m] += Vx[i] * r[R::HXX + i * NX * NX + m];
