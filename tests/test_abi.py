@@ -176,7 +176,8 @@ def test_ddp_queries_and_argument_errors_without_gpu():
     """noc_ddp_*: workspace size, family support (nx <= 4) and argument validation are host logic."""
     from noc import _lib, problems
     lib = _lib.load()
-    rec = 16 + 4 + 4 + 1 + 1 + 4 * (16 + 4 + 1)   # fx fu cx cu cuu | d2f_i (xx, xu, uu) per i
+    # fx fu cx cu | cxx cuu cxu (the stage cost's Hessian) | d2f_i (xx, xu, uu) per i
+    rec = 16 + 4 + 4 + 1 + (16 + 1 + 4) + 4 * (16 + 4 + 1)
     assert lib.noc_ddp_work_doubles(4, 1, 200, 3) == 3 * (2 * 201 * 4 + 2 * 200 + 200 * 4 + 200 * rec)
     assert lib.noc_ddp_work_doubles(0, 1, 10, 1) < 0
     for ocp, ok in ((problems.pendulum(0.02), 1), (problems.cartpole(0.005), 1),
