@@ -36,7 +36,8 @@
 extern "C" {
 #endif
 
-#define NOC_ABI_VERSION 3 /* 2: noc_ipm_ws gained `repeats`; 3: `order` */
+#define NOC_ABI_VERSION 4 /* 2: noc_ipm_ws gained `repeats`; 3: `order`; 4: noc_check_feasibility,
+                             noc_ddp_solve_ex, noc_ddp_bwd_pass, noc_nonlin_rollout (additive) */
 
 /* Library identity / diagnostics. */
 int noc_abi_version(void);
@@ -281,6 +282,33 @@ int noc_ddp_supported(const noc_family* fam);
 int noc_ddp_solve(const noc_family* fam, int N, int Bt, const double* x0, double* u, double* work,
                   int* iterations, int* passes, int* done, double bp0, int max_passes,
                   void* stream);
+/* noc_ddp_solve with flags: NOC_DDP_ONE_STAGE = ddp(ocp, controls, initial_state, barrier_param)
+ * (noc/differential_dynamic_programming.py:98-186): the DDP iterations at bp0 only, no barrier
+ * schedule; iterations[b] = that stage's DDP iterations, work starts with its final states. */
+#define NOC_DDP_ONE_STAGE 1
+int noc_ddp_solve_ex(const noc_family* fam, int N, int Bt, const double* x0, double* u,
+                     double* work, int* iterations, int* passes, int* done, double bp0,
+                     int max_passes, int flags, void* stream);
+/* bwd_pass(final_cost, final_state, d, reg_param) of the DDP module
+ * (noc/differential_dynamic_programming.py:28-70): the second-order backward pass (Q-function
+ * with the Vx . fxx / fxu / fuu terms) from Vx = grad(final_cost)(x_N) (B, nx), Vxx =
+ * hessian(final_cost)(x_N) (B, nx, nx) (noc_final_cost_derivs) over the Derivatives arrays of
+ * noc_derivatives (natural layout, B leading); reg = reg_param[b] * ||cu_b||_F added to Quu.
+ * Outputs ffgain k (B, N, nu), gain K (B, N, nu, nx), pred (B) = sum dV, feasible (B) int32 =
+ * all eigh(Quu) > 0, Hu (B, N, nu) = Qu.  (nx, nu) as noc_kkt_supported; one thread per
+ * trajectory (the recursion is nonlinear in V: no scan). */
+int noc_ddp_bwd_pass(int nx, int nu, int N, int B, const double* Vx, const double* Vxx,
+                     const double* reg_param, const double* cx, const double* cu,
+                     const double* cxx, const double* cuu, const double* cxu, const double* fx,
+                     const double* fu, const double* fxx, const double* fuu, const double* fxu,
+                     double* k, double* K, double* pred, int* feasible, double* Hu, void* stream);
+/* nonlin_rollout(ocp, gain, ffgain, nominal_states, nominal_controls)
+ * (noc/differential_dynamic_programming.py:73-90 == noc/par_interior_point_newton.py:87-104):
+ * x_hat_0 = x_0, u_hat_s = u_s + k_s + K_s (x_hat_s - x_s), x_hat_{s+1} = dynamics(x_hat_s,
+ * u_hat_s).  K (B, N, nu, nx), k (B, N, nu), x (B, N+1, nx), u (B, N, nu) -> x_new, u_new. */
+int noc_nonlin_rollout(const noc_family* fam, int N, int B, const double* K, const double* k,
+                       const double* x, const double* u, double* x_new, double* u_new,
+                       void* stream);
 
 #ifdef __cplusplus
 }

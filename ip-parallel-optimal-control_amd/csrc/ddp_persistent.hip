@@ -39,6 +39,7 @@ __device__ int g_ddp_trace_traj = 0;
 struct DdpArgs {
   int N, Bt, max_passes;
   int skip_repeats;  // account the identical retries at the rp clip without recomputing them
+  int one_stage;     // NOC_DDP_ONE_STAGE: ddp(ocp, u, x0, bp) -- one barrier value (D:98-186)
   double bp0;
   const double* x0;
   double* u;
@@ -334,6 +335,7 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
     }
     total_it += it;  // D:196
     bp = bp / 5.0;   // D:195
+    if (a.one_stage) break;
   }
   // the final controls / states may live in the trial buffers: copy them out (lane-parallel)
   if (U != ubuf) for (int i = l; i < N * NU; i += 64) ubuf[i] = U[i];
@@ -371,8 +373,9 @@ long long ddp_record_doubles(int nx, int nu) {
 
 hipError_t ddp_solve(const noc_family& p, int N, int Bt, const double* x0, double* u,
                      double* work, int* iterations, int* passes, int* done, double bp0,
-                     int max_passes, hipStream_t s) {
+                     int max_passes, int flags, hipStream_t s) {
   DdpArgs a{};
+  a.one_stage = (flags & NOC_DDP_ONE_STAGE) ? 1 : 0;
   a.N = N;
   a.Bt = Bt;
   a.max_passes = max_passes;

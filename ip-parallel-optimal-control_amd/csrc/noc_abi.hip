@@ -392,6 +392,14 @@ int noc_ddp_supported(const noc_family* fam) { return (fam && noc::ddp_supported
 int noc_ddp_solve(const noc_family* fam, int N, int Bt, const double* x0, double* u, double* work,
                   int* iterations, int* passes, int* done, double bp0, int max_passes,
                   void* stream) {
+  return noc_ddp_solve_ex(fam, N, Bt, x0, u, work, iterations, passes, done, bp0, max_passes, 0,
+                          stream);
+}
+
+int noc_ddp_solve_ex(const noc_family* fam, int N, int Bt, const double* x0, double* u,
+                     double* work, int* iterations, int* passes, int* done, double bp0,
+                     int max_passes, int flags, void* stream) {
+  if (flags & ~NOC_DDP_ONE_STAGE) return fail(-1, "ddp flags: only NOC_DDP_ONE_STAGE is defined");
   if (!fam) return fail(-2, "family is NULL");
   if (!noc::ddp_supported(*fam))
     return fail(-1, "DDP supports the registered families with nx <= 4 (noc_ddp_supported)");
@@ -406,7 +414,45 @@ int noc_ddp_solve(const noc_family* fam, int N, int Bt, const double* x0, double
     return rc;
   if (Bt == 0) return 0;
   return hip_status(noc::ddp_solve(*fam, N, Bt, x0, u, work, iterations, passes, done, bp0,
-                                   max_passes, static_cast<hipStream_t>(stream)), "ddp_solve");
+                                   max_passes, flags, static_cast<hipStream_t>(stream)), "ddp_solve");
+}
+
+int noc_ddp_bwd_pass(int nx, int nu, int N, int B, const double* Vx, const double* Vxx,
+                     const double* reg_param, const double* cx, const double* cu,
+                     const double* cxx, const double* cuu, const double* cxu, const double* fx,
+                     const double* fu, const double* fxx, const double* fuu, const double* fxu,
+                     double* k, double* K, double* pred, int* feasible, double* Hu, void* stream) {
+  if (!noc::kkt_supported(nx, nu))
+    return fail(-1, "noc_ddp_bwd_pass: unsupported (nx, nu); supported: " + noc::kkt_shapes_str());
+  if (N < 1 || B < 0) return fail(-1, "need N >= 1, B >= 0");
+  const void* req[] = {Vx, Vxx, reg_param, cx, cu, cxx, cuu, cxu, fx, fu, fxx, fuu, fxu, k, K,
+                       pred, Hu};
+  for (const void* p : req) {
+    int rc = check_ptr(p, "ddp_bwd_pass argument", true, 8);
+    if (rc) return rc;
+  }
+  int rc = check_ptr(feasible, "feasible", true, 4);
+  if (rc) return rc;
+  if (B == 0) return 0;
+  noc::DdpBwdArgs a{N, B, Vx, Vxx, reg_param, cx, cu, cxx, cuu, cxu, fx, fu, fxx, fuu, fxu,
+                    k, K, pred, Hu, feasible};
+  return hip_status(noc::ddp_bwd_pass(nx, nu, a, static_cast<hipStream_t>(stream)), "ddp_bwd_pass");
+}
+
+int noc_nonlin_rollout(const noc_family* fam, int N, int B, const double* K, const double* k,
+                       const double* x, const double* u, double* x_new, double* u_new,
+                       void* stream) {
+  if (!fam) return fail(-2, "family is NULL");
+  if (!noc::family_supported(*fam)) return fail(-1, "unsupported problem family (kind/nx/nu)");
+  if (N < 1 || B < 0) return fail(-1, "need N >= 1, B >= 0");
+  const void* req[] = {K, k, x, u, x_new, u_new};
+  for (const void* p : req) {
+    int rc = check_ptr(p, "nonlin_rollout argument", true, 8);
+    if (rc) return rc;
+  }
+  if (B == 0) return 0;
+  return hip_status(noc::nonlin_rollout(*fam, N, B, K, k, x, u, x_new, u_new,
+                                        static_cast<hipStream_t>(stream)), "nonlin_rollout");
 }
 
 int noc_derivatives(const noc_family* fam, int N, int B, const double* x, const double* u,

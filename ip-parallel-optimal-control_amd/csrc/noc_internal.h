@@ -158,7 +158,18 @@ bool ddp_supported(const noc_family& p);
 long long ddp_record_doubles(int nx, int nu);
 hipError_t ddp_solve(const noc_family& p, int N, int Bt, const double* x0, double* u,
                      double* work, int* iterations, int* passes, int* done, double bp0,
-                     int max_passes, hipStream_t s);
+                     int max_passes, int flags, hipStream_t s);
+// DDP building blocks (ddp_blocks.hip)
+struct DdpBwdArgs {
+  int N, B;
+  const double *Vx, *Vxx, *reg_param;
+  const double *cx, *cu, *cxx, *cuu, *cxu, *fx, *fu, *fxx, *fuu, *fxu;
+  double *k, *K, *pred, *Hu;
+  int* feasible;
+};
+hipError_t ddp_bwd_pass(int nx, int nu, const DdpBwdArgs& a, hipStream_t s);
+hipError_t nonlin_rollout(const noc_family& p, int N, int B, const double* K, const double* k,
+                          const double* x, const double* u, double* xn, double* un, hipStream_t s);
 int debug_phase_cycles(long long* out, int n, int reset);
 int debug_traj_times(long long* out, int n);
 hipError_t ipm_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal, double bp0,

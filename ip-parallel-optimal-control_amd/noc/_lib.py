@@ -25,6 +25,7 @@ KKT_KERNEL_SOURCES = {
     + _COMMON_SOURCES,
 }
 
+ABI_VERSION = 4  # include/noc_hip.h NOC_ABI_VERSION
 _dp = ctypes.c_void_p  # device pointers are passed as opaque addresses
 _i = ctypes.c_int
 
@@ -51,6 +52,7 @@ PHASE_ROLLOUT, PHASE_LINEARIZE, PHASE_SOLVE, PHASE_DONE, PHASE_ROLLED = 0, 1, 2,
 PHASE_ROLLOUT_PENDING = 5
 MODE_PAR, MODE_SEQ = 0, 1
 TERMINAL_FINAL_COST, TERMINAL_STAGE0 = 0, 1
+DDP_ONE_STAGE = 1  # noc_ddp_solve_ex flags bit: ddp() at one barrier value
 
 
 class NocFamily(ctypes.Structure):
@@ -104,6 +106,9 @@ SIGNATURES.update({
     "noc_ddp_work_doubles": (ctypes.c_longlong, [_i, _i, _i, _i]),
     "noc_ddp_supported": (_i, [_fp]),
     "noc_ddp_solve": (_i, [_fp, _i, _i] + [_dp] * 6 + [ctypes.c_double, _i, _dp]),
+    "noc_ddp_solve_ex": (_i, [_fp, _i, _i] + [_dp] * 6 + [ctypes.c_double, _i, _i, _dp]),
+    "noc_ddp_bwd_pass": (_i, [_i] * 4 + [_dp] * 18 + [_dp]),
+    "noc_nonlin_rollout": (_i, [_fp, _i, _i] + [_dp] * 6 + [_dp]),
 })
 
 _lib: Optional[ctypes.CDLL] = None
@@ -120,7 +125,7 @@ def _typed(lib: ctypes.CDLL) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.noc_abi_version() != 3:
+    if lib.noc_abi_version() != ABI_VERSION:
         raise NocError("libnoc_hip.so ABI version mismatch")
     return lib
 

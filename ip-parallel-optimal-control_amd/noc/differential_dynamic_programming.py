@@ -10,6 +10,12 @@ evaluated lane-parallel).  Differences, all additive:
     result is then batched too -- each trajectory follows its own reference control flow;
   * `ocp.family` must be a registered family with nx <= 4 (noc.problems);
   * return_info=True adds the backward-pass counts (incl. rejected retries) and final states.
+
+The module's building blocks keep the reference names too (D:10-186): compute_derivatives (the
+same jax.grad / hessian / jacrev arrays as the Newton solvers', noc_derivatives), bwd_pass (the
+second-order backward pass, noc_ddp_bwd_pass), nonlin_rollout (noc_nonlin_rollout),
+check_feasibility (noc_check_feasibility) and ddp (one barrier value, noc_ddp_solve_ex with
+NOC_DDP_ONE_STAGE).
 """
 from __future__ import annotations
 
@@ -18,12 +24,78 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from .optimal_control_problem import OCP
+from .optimal_control_problem import OCP, Derivatives
+from .par_interior_point_newton import (_dev, _family, check_traj_feasibility,
+                                        compute_derivatives, nonlin_rollout)
+
+__all__ = ["compute_derivatives", "bwd_pass", "nonlin_rollout", "check_feasibility", "ddp",
+           "interior_point_ddp"]
+
+
+def check_feasibility(ocp: OCP, x, u):
+    """D:93-95 (== P:45-47)."""
+    return check_traj_feasibility(ocp, x, u)
+
+
+def bwd_pass(final_cost, final_state, d: Derivatives, reg_param):
+    """D:28-70: the DDP backward pass -> (ffgain k (N, nu), gain K (N, nu, nx), pred_reduction,
+    feasible_bwd_pass, Hu (N, nu)).  Vx, Vxx at x_N are grad / hessian of `final_cost` (the OCP's
+    callable, carrying its family, or the OCP itself); reg = reg_param * ||cu||_F.  Batched inputs
+    (leading B axis) give batched outputs."""
+    import torch
+    from .costates import final_cost_grad
+    fam = getattr(final_cost, "family", None)
+    if fam is None:
+        raise _lib.NocError("bwd_pass: final_cost must be a registered family's callable (or its "
+                            "OCP): grad / hessian come from the device code")
+
+    class _O:  # noqa: N801 -- the family-bearing stand-in final_cost_grad expects
+        family = fam
+    xN = _dev(final_state, "final_state")
+    dd = Derivatives(*(_dev(t) for t in d))
+    single = dd.cu.dim() == 2
+    if single:
+        xN = xN[None]
+        dd = Derivatives(*(t[None] for t in dd))
+    Vx, Vxx = final_cost_grad(_O, xN, hessian=True)
+    B, N, nu = dd.cu.shape
+    nx = dd.cx.shape[-1]
+    dev = dd.cu.device
+    f64 = dict(dtype=torch.float64, device=dev)
+    rp = torch.as_tensor(reg_param, **f64).reshape(-1).expand(B).contiguous()
+    k, K, pred, Hu = (torch.empty(s, **f64) for s in ((B, N, nu), (B, N, nu, nx), (B,), (B, N, nu)))
+    feas = torch.empty(B, dtype=torch.int32, device=dev)
+    lib = _lib.for_shape(nx, nu)
+    _lib.check(lib.noc_ddp_bwd_pass(nx, nu, N, B, Vx.data_ptr(), Vxx.contiguous().data_ptr(),
+                                    rp.data_ptr(), *(getattr(dd, f).data_ptr() for f in
+                                                     Derivatives._fields),
+                                    k.data_ptr(), K.data_ptr(), pred.data_ptr(), feas.data_ptr(),
+                                    Hu.data_ptr(), _lib.stream_handle(dev)),
+               "noc_ddp_bwd_pass", lib)
+    res = (k, K, pred, feas.bool(), Hu)
+    return tuple(t[0] for t in res) if single else res
+
+
+def ddp(ocp: OCP, controls, initial_state, barrier_param, device="cuda",
+        max_passes: int = 10 ** 7):
+    """D:98-186: ONE barrier value -- rollout, then DDP iterations with the retry loop until
+    |Hu|inf < 1e-4 (or 500 iterations) -> (states, controls, iterations)."""
+    X, U, its, _ = _solve(ocp, controls, initial_state, device, float(barrier_param), max_passes,
+                          _lib.DDP_ONE_STAGE)
+    return X, U, its
 
 
 def interior_point_ddp(ocp: OCP, controls, initial_state, device="cuda", bp0: float = 0.1,
                        max_passes: int = 10 ** 7, return_info: bool = False):
     """D:189-208: barrier 0.1 / 5^k while > 1e-4, ddp (D:98-186) at each barrier value."""
+    X, Uh, itn, info = _solve(ocp, controls, initial_state, device, float(bp0), max_passes, 0)
+    if return_info:
+        info["states"] = X
+        return Uh, itn, info
+    return Uh, itn
+
+
+def _solve(ocp, controls, initial_state, device, bp0, max_passes, flags):
     import torch
     if ocp.family is None:
         raise _lib.NocError("OCP has no registered device family (use noc.problems.*): the HIP "
@@ -48,16 +120,15 @@ def interior_point_ddp(ocp: OCP, controls, initial_state, device="cuda", bp0: fl
     work = torch.empty(int(lib.noc_ddp_work_doubles(nx, nu, N, Bt)), **f64)
     i32 = dict(device=dev, dtype=torch.int32)
     its, passes, done = (torch.zeros(Bt, **i32) for _ in range(3))
-    _lib.check(lib.noc_ddp_solve(ctypes.byref(fam), N, Bt, _lib.ptr(X0), _lib.ptr(U),
-                                 _lib.ptr(work), _lib.ptr(its), _lib.ptr(passes), _lib.ptr(done),
-                                 float(bp0), int(max_passes), _lib.stream_handle(dev)),
-               "noc_ddp_solve", lib)
+    _lib.check(lib.noc_ddp_solve_ex(ctypes.byref(fam), N, Bt, _lib.ptr(X0), _lib.ptr(U),
+                                    _lib.ptr(work), _lib.ptr(its), _lib.ptr(passes),
+                                    _lib.ptr(done), float(bp0), int(max_passes), int(flags),
+                                    _lib.stream_handle(dev)),
+               "noc_ddp_solve_ex", lib)
     Uh, itn = U.cpu().numpy(), its.cpu().numpy()
-    info = dict(passes=passes.cpu().numpy(), done=done.cpu().numpy().astype(bool),
-                states=work[:Bt * (N + 1) * nx].view(Bt, N + 1, nx).cpu().numpy())
+    X = work[:Bt * (N + 1) * nx].view(Bt, N + 1, nx).cpu().numpy()
+    info = dict(passes=passes.cpu().numpy(), done=done.cpu().numpy().astype(bool))
     if single:
-        Uh, itn = Uh[0], int(itn[0])
+        Uh, itn, X = Uh[0], int(itn[0]), X[0]
         info = {k: v[0] for k, v in info.items()}
-    if return_info:
-        return Uh, itn, info
-    return Uh, itn
+    return X, Uh, itn, info

@@ -1,8 +1,8 @@
 """Parallel-in-time interior-point solver -- drop-in for noc/par_interior_point_newton.py.
 
 Every public function of the reference module is here with its signature (P:13-254):
-compute_derivatives, compute_lqr_params, check_traj_feasibility, noc_to_lqt, par_Newton,
-newton_oc, par_interior_point_optimal_control.  They run on the MI355X: the building blocks as
+compute_derivatives, compute_lqr_params, check_traj_feasibility, noc_to_lqt, nonlin_rollout,
+par_Newton, newton_oc, par_interior_point_optimal_control.  They run on the MI355X: the building blocks as
 batched HIP kernels (noc_derivatives, noc_costates, noc_lqr_params, noc_kkt_solve), the loops as
 the persistent whole-solve kernel (noc_ipm_solve) or the launch-per-phase driver.
 
@@ -117,6 +117,25 @@ def check_traj_feasibility(ocp: OCP, x, u):
                "noc_check_feasibility", lib)
     ok = ok.bool()
     return ok[0] if single else ok
+
+
+def nonlin_rollout(ocp: OCP, gain, ffgain, nominal_states, nominal_controls):
+    """P:87-104 (== D:73-90): x_hat_0 = x_0, u_hat = u + k + K (x_hat - x), x_hat+ =
+    dynamics(x_hat, u_hat) -> (new_states (N+1, nx), new_controls (N, nu)); batched inputs
+    (leading B axis) give batched outputs (noc_nonlin_rollout, one thread per trajectory)."""
+    fam = _family(ocp)
+    K, k = _dev(gain, "gain"), _dev(ffgain, "ffgain")
+    x, u = _dev(nominal_states, "nominal_states"), _dev(nominal_controls, "nominal_controls")
+    single = u.dim() == 2
+    if single:
+        K, k, x, u = K[None], k[None], x[None], u[None]
+    B, N = u.shape[0], u.shape[1]
+    xn, un = torch.empty_like(x), torch.empty_like(u)
+    lib = _lib.load_for(fam)
+    _lib.check(lib.noc_nonlin_rollout(ctypes.byref(fam.to_c()), N, B, K.data_ptr(), k.data_ptr(),
+                                      x.data_ptr(), u.data_ptr(), xn.data_ptr(), un.data_ptr(),
+                                      _lib.stream_handle(u.device)), "noc_nonlin_rollout", lib)
+    return (xn[0], un[0]) if single else (xn, un)
 
 
 def noc_to_lqt(ru, Q, R, M, A, B):

@@ -166,3 +166,77 @@ def test_ddp_gpu_retry_repeats_accounted_bit_identical(case, monkeypatch):
         assert np.array_equal(pa, pb) and np.array_equal(da, db)
     if case == "linear":
         assert np.all(res["1", 10 ** 7][2] >= 501)  # a cap-length retry loop happened
+
+
+# ------------------------------------------------------------------------------------------------
+# the DDP module's building blocks (D:10-186) with the reference names
+# ------------------------------------------------------------------------------------------------
+def _nominal(name, N, B, seed):
+    from noc import problems
+    from noc.utils import rollout
+    ocp = _device_problem(name, N)
+    x0, u0 = problems.initial_conditions(name if name != "linear2" else "pendulum", N, B, seed=seed)
+    X = np.stack([rollout(ocp.dynamics, u0[b], x0[b]) for b in range(B)])
+    return ocp, X, u0, x0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,N", [("pendulum", 40), ("cartpole", 30)])
+def test_ddp_bwd_pass_and_nonlin_rollout_match_oracle(name, N):
+    """bwd_pass (D:28-70, noc_ddp_bwd_pass) on the device derivatives against the oracle's
+    restatement on torch.func derivatives: k, K, Hu, pred at 1e-9 relative, identical feasibility
+    flags; nonlin_rollout (D:73-90 == P:87-104, noc_nonlin_rollout) at 1e-12; batched and
+    unbatched; reg_param per trajectory."""
+    from noc import differential_dynamic_programming as D
+    from noc.par_interior_point_newton import nonlin_rollout as par_nonlin_rollout
+    from oracle import noc_oracle as O
+    B = 3
+    ocp, X, U, _ = _nominal(name, N, B, 17)
+    prob = _oracle_problem(name, N)
+    bp, rps = 0.1, np.array([1.0, 1e-3, 25.0])
+    d = D.compute_derivatives(ocp, X, U, bp)
+    k, K, pred, feas, Hu = D.bwd_pass(ocp.final_cost, X[:, -1], d, rps)
+    k, K, pred, feas, Hu = (t.cpu().numpy() for t in (k, K, pred, feas, Hu))
+    for b in range(B):
+        derivs = prob.derivatives(X[b], U[b], bp)
+        Vx, Vxx = prob.final_grad_hess(X[b, -1])
+        kr, Kr, pr, fr, Hr = O.ddp_bwd_pass(Vx, Vxx, derivs, rps[b])
+        rel = lambda a, r: float(np.max(np.abs(a - r)) / max(1.0, float(np.max(np.abs(r)))))
+        assert rel(k[b], kr) < 1e-9 and rel(K[b], Kr) < 1e-9 and rel(Hu[b], Hr) < 1e-9, b
+        assert abs(pred[b] - pr) <= 1e-9 * max(1.0, abs(pr)) and bool(feas[b]) == fr
+        one = D.bwd_pass(ocp, X[b, -1], type(d)(*(t[b] for t in d)), rps[b])
+        assert np.array_equal(one[0].cpu().numpy(), k[b])
+        TX, TU = D.nonlin_rollout(ocp, Kr, kr, X[b], U[b])
+        TXr, TUr = O.ddp_nonlin_rollout(prob, Kr, kr, X[b], U[b])
+        assert rel(TX.cpu().numpy(), TXr) < 1e-12 and rel(TU.cpu().numpy(), TUr) < 1e-12
+    TXb, TUb = par_nonlin_rollout(ocp, K, k, X, U)
+    assert TXb.shape == X.shape and TUb.shape == U.shape
+    TX0, _ = D.nonlin_rollout(ocp, K[0], k[0], X[0], U[0])
+    assert np.array_equal(TXb[0].cpu().numpy(), TX0.cpu().numpy())
+
+
+@pytest.mark.gpu
+def test_ddp_one_stage_matches_oracle_and_chains_to_interior_point_ddp():
+    """ddp(ocp, controls, initial_state, barrier_param) (D:98-186: one barrier value,
+    noc_ddp_solve_ex with NOC_DDP_ONE_STAGE) against the oracle's ddp (iterations within one,
+    states / controls 1e-5); chained over the schedule 0.1 / 5^k it reproduces
+    interior_point_ddp bit for bit (same kernel, one stage per call)."""
+    from noc import differential_dynamic_programming as D
+    from noc import problems
+    from oracle import noc_oracle as O
+    N = 30
+    ocp = problems.pendulum(1.0 / N)
+    x0, u0 = problems.initial_conditions("pendulum", N, 2, seed=23)
+    X, U, its = D.ddp(ocp, u0, x0, 0.1)
+    prob = _oracle_problem("pendulum", N)
+    for b in range(2):
+        Xr, Ur, itr, _ = O.ddp(prob, u0[b], x0[b], 0.1)
+        assert abs(int(its[b]) - itr) <= 1
+        assert np.max(np.abs(U[b] - Ur)) < 1e-5 and np.max(np.abs(X[b] - Xr)) < 1e-5
+    Uc, total, bp = u0, np.zeros(2, dtype=int), 0.1
+    while bp > 1e-4:
+        _, Uc, it = D.ddp(ocp, Uc, x0, bp)
+        total += it
+        bp = bp / 5
+    Uf, itf = D.interior_point_ddp(ocp, u0, x0)
+    assert np.array_equal(Uc, Uf) and np.array_equal(total, itf)
