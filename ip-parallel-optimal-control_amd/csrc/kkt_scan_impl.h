@@ -405,14 +405,14 @@ NOC_DEV void combine_sklansky(Elem<NX>& e1) {
 
 // Phase 2 as a reverse Sklansky scan over an L-lane segment: log2(L) levels, partners on the VALU;
 // the last level's partner (lane L/2 of the segment) covers the terminal cost -> value-only.
-template <int NX, int L, int K = 0>
+template <int NX, int L, int K = 0, bool MASKED = (NX <= 2)>
 NOC_DEV void rev_scan_sklansky(Elem<NX>& e) {
   NOC_ISA_MARK("rev", K);
   if constexpr ((2 << K) < L) {
-    combine_sklansky<NX, false, K>(e);
-    rev_scan_sklansky<NX, L, K + 1>(e);
+    combine_sklansky<NX, false, K, MASKED>(e);
+    rev_scan_sklansky<NX, L, K + 1, MASKED>(e);
   } else if constexpr ((2 << K) == L) {
-    combine_sklansky<NX, true, K>(e);
+    combine_sklansky<NX, true, K, MASKED>(e);
     NOC_ISA_MARK("rev", K + 1);
   }
 }
@@ -518,7 +518,9 @@ struct ArgsSrc {
 // HANDOFF: phase 3 hands the chunk's first stage (A, B) to phase 4 in registers (standalone
 // scan: −1 stage of phase 4's re-reads); off inside the persistent solver, whose register budget
 // it would push into scratch (444 -> 516 B/lane).
-template <int NX, int NU, int L, bool AFF, bool TILED, class SRC, int CACHE = 0, bool HANDOFF = true>
+// BIG: the instance owns a SIMD (512 registers): the combines run masked (no identity partner).
+template <int NX, int NU, int L, bool AFF, bool TILED, class SRC, int CACHE = 0, bool HANDOFF = true,
+          bool BIG = false>
 NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, const SRC& src) {
   constexpr int KD = kd_width<NX, NU>();
   if (traj >= a.B) return;                     // uniform over the segment
@@ -593,7 +595,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     NOC_STAMP(1); NOC_ISA_MARK("phase", 1);
     // ---------------- phase 2: reverse Sklansky scan across lanes ----------------
     if constexpr (W == 1) {
-      if (!(a.ablate & 1)) rev_scan_sklansky<NX, L>(e);
+      if (!(a.ablate & 1)) rev_scan_sklansky<NX, L, 0, (NX <= 2 || BIG)>(e);
     } else {
       if (!(a.ablate & 1)) {
         // per wave; wave 1 ends at the terminal cost (value-only last level), wave 0 at wave 1's
@@ -1010,16 +1012,19 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   NOC_STAMP(6);
 }
 
-template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE = 0, bool HANDOFF = true>
+template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE = 0, bool HANDOFF = true,
+          bool BIG = false>
 NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
   const int cmax = a.N / L + (a.N % L ? 1 : 0);
   const ArgsSrc<NX, NU, L, AFF, TILED> src{a, traj, l, cmax, (size_t)traj * a.N};
-  kkt_scan_wave_src<NX, NU, L, AFF, TILED, ArgsSrc<NX, NU, L, AFF, TILED>, CACHE, HANDOFF>(a, traj, l,
+  kkt_scan_wave_src<NX, NU, L, AFF, TILED, ArgsSrc<NX, NU, L, AFF, TILED>, CACHE, HANDOFF, BIG>(a, traj, l,
                                                                                           src);
 }
 
-template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE>
-__global__ __launch_bounds__(L > 64 ? L : 256, L > 64 ? 1 : NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
+// BIG (L <= 64): one wave per SIMD -- for batches whose waves all fit one per SIMD anyway (the
+// 1024-per-GPU shard): 512 registers (no spill) and masked combines, like the two-wave segments.
+template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE, bool BIG = false>
+__global__ __launch_bounds__(L > 64 ? L : 256, (L > 64 || BIG) ? 1 : NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   // Two-wave segments (L = 128) must put their two waves on DIFFERENT SIMDs: with <= 256
   // registers per wave the dispatcher placed both waves of a 128-thread block on one SIMD (their
@@ -1028,7 +1033,7 @@ __global__ __launch_bounds__(L > 64 ? L : 256, L > 64 ? 1 : NOC_KKT_WAVES_PER_SI
   // included: no wave of this kernel can share a SIMD) makes the two waves of a block land on two
   // SIMDs; the launch policy (kkt_pick_lanes) uses L = 128 only when every wave is then resident
   // at once (B * 2 <= #SIMDs).
-  if constexpr (L > 64) asm volatile("" ::: "a255");
+  if constexpr (L > 64 || BIG) asm volatile("" ::: "a255");
   const int traj = tid / L;
   if constexpr (L <= 64) {
     // a wave with no trajectory to solve (past the batch, or masked off) still meets the one
@@ -1040,7 +1045,7 @@ __global__ __launch_bounds__(L > 64 ? L : 256, L > 64 ? 1 : NOC_KKT_WAVES_PER_SI
       return;
     }
   }
-  kkt_scan_wave<NX, NU, L, AFF, TILED, CACHE>(a, traj, tid % L);
+  kkt_scan_wave<NX, NU, L, AFF, TILED, CACHE, true, BIG>(a, traj, tid % L);
 }
 
 // Register-cached chunk length for (NX, NU, L): only where a short chunk's blocks fit beside the
@@ -1069,11 +1074,21 @@ hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
   constexpr int CC = kkt_cache_len<NX, NU, L>();
   const int cmax = a.N / L + (a.N % L ? 1 : 0);
   const bool cached = CC > 0 && cmax <= CC && !(a.ablate & 8);  // ablation bit 3: streamed chunks
+  // the batch's waves fit one per SIMD: the 512-register instance (NOC_KKT_BIG=0 disables)
+  const bool big = L == 64 && NX >= 3 && NX <= 4 && (threads + 63) / 64 <= kkt_device_simds() &&
+                   kkt_big_enabled();
   if (cached) {
     if (a.tiled)
       hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, CC>), dim3(grid), dim3(block), lds, stream, a);
     else
       hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, false, CC>), dim3(grid), dim3(block), lds, stream, a);
+  } else if (big) {
+    if constexpr (L == 64 && NX >= 3 && NX <= 4) {
+      if (a.tiled)
+        hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, 0, true>), dim3(grid), dim3(block), lds, stream, a);
+      else
+        hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, false, 0, true>), dim3(grid), dim3(block), lds, stream, a);
+    }
   } else {
     if (a.tiled)
       hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, 0>), dim3(grid), dim3(block), lds, stream, a);

@@ -67,6 +67,16 @@ inline int kkt_waves_per_block(long waves, size_t lds_per_wave) {
   return w;
 }
 
+// The one-wave-per-SIMD (512-register) L = 64 scan instance for batches whose waves fit one per
+// SIMD (kkt_scan_impl.h: BIG); NOC_KKT_BIG=0 turns it off (read once).
+inline bool kkt_big_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NOC_KKT_BIG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 inline size_t kkt_lds_bytes_rt(int nx, int nu, int N, int L) {
   if (L < 8) return 0;  // lanes = 1 (group solve): gains go through HBM
   const size_t per_traj = (size_t)(((long long)N * nu * (nx + 1) + nx + 1) & ~1LL);
