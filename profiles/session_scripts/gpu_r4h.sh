@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 4, session h: masked combines in the one-wave-per-SIMD persistent instance (cart-pole,
+# WPS = 1): interleaved A/B against the committed build (libnoc_hip_old.so) on whole solves that
+# run that instance -- cart-pole N = 200 B = 1024 and N = 100 B = 1 -- with the u hash (results
+# must be identical), then the IPM tests.
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+cd "$R"; O=gpurun_out/${OUT:-r4h}; mkdir -p $O
+export TMPDIR=/tmp
+L="$R/ip-parallel-optimal-control_amd/noc/_lib"
+run() { local ok=$1; local t=$2; local log=$3; shift 3; timeout -k 10 "$t" "$@" > "$O/$log" 2>&1; local rc=$?; echo "rc=$rc $log"; tail -1 "$O/$log" | cut -c1-260; if [ $rc -ne 0 ] && [ $rc -ne $ok ]; then exit $rc; fi; }
+for i in 1 2 3; do
+  NOC_HIP_LIB=$L/libnoc_hip_old.so run 0 200 old_b1024_$i.txt python tools/ipm_bench.py cartpole 200 1024 persistent
+  run 0 200 new_b1024_$i.txt python tools/ipm_bench.py cartpole 200 1024 persistent
+  NOC_HIP_LIB=$L/libnoc_hip_old.so run 0 200 old_b1_$i.txt python tools/ipm_bench.py cartpole 100 1 persistent
+  run 0 200 new_b1_$i.txt python tools/ipm_bench.py cartpole 100 1 persistent
+done
+run 1 900 pytest.txt python -u -m pytest tests/test_ipm_gpu.py tests/test_api_gpu.py tests/test_golden_gpu.py -m gpu -q --timeout 300 --timeout-method thread -rf
