@@ -1021,8 +1021,9 @@ NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
                                                                                           src);
 }
 
-// BIG (L <= 64): one wave per SIMD -- for batches whose waves all fit one per SIMD anyway (the
-// 1024-per-GPU shard): 512 registers (no spill) and masked combines, like the two-wave segments.
+// BIG (L = 32, 64; nx = 3, 4): one wave per SIMD -- for batches whose waves all fit one per SIMD
+// anyway (the 2048- and 1024-per-GPU shards): 512 registers (no spill) and masked combines, like
+// the two-wave segments.
 template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE, bool BIG = false>
 __global__ __launch_bounds__(L > 64 ? L : 256, (L > 64 || BIG) ? 1 : NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1075,15 +1076,15 @@ hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
   const int cmax = a.N / L + (a.N % L ? 1 : 0);
   const bool cached = CC > 0 && cmax <= CC && !(a.ablate & 8);  // ablation bit 3: streamed chunks
   // the batch's waves fit one per SIMD: the 512-register instance (NOC_KKT_BIG=0 disables)
-  const bool big = L == 64 && NX >= 3 && NX <= 4 && (threads + 63) / 64 <= kkt_device_simds() &&
-                   kkt_big_enabled();
+  const bool big = (L == 64 || L == 32) && NX >= 3 && NX <= 4 &&
+                   (threads + 63) / 64 <= kkt_device_simds() && kkt_big_enabled();
   if (cached) {
     if (a.tiled)
       hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, CC>), dim3(grid), dim3(block), lds, stream, a);
     else
       hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, false, CC>), dim3(grid), dim3(block), lds, stream, a);
   } else if (big) {
-    if constexpr (L == 64 && NX >= 3 && NX <= 4) {
+    if constexpr ((L == 64 || L == 32) && NX >= 3 && NX <= 4) {
       if (a.tiled)
         hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, 0, true>), dim3(grid), dim3(block), lds, stream, a);
       else
