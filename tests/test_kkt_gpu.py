@@ -77,7 +77,7 @@ def test_kkt_infeasible_flag(lanes):
     assert relerr(out["dx"][ok], ref["dx"][ok]) < RTOL
 
 
-@pytest.mark.parametrize("lanes", [0, 1, 128])
+@pytest.mark.parametrize("lanes", [0, 1, 32, 64, 128])
 def test_kkt_active_mask_leaves_inactive_untouched(lanes):
     from noc import lqt
     case = rand_lq(11, 6, 40, 4, 1)
