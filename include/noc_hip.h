@@ -36,8 +36,9 @@
 extern "C" {
 #endif
 
-#define NOC_ABI_VERSION 4 /* 2: noc_ipm_ws gained `repeats`; 3: `order`; 4: noc_check_feasibility,
-                             noc_ddp_solve_ex, noc_ddp_bwd_pass, noc_nonlin_rollout (additive) */
+#define NOC_ABI_VERSION 5 /* 2: noc_ipm_ws gained `repeats`; 3: `order`; 4: noc_check_feasibility,
+                             noc_ddp_solve_ex, noc_ddp_bwd_pass, noc_nonlin_rollout (additive);
+                             5: noc_total_cost (additive) */
 
 /* Library identity / diagnostics. */
 int noc_abi_version(void);
@@ -268,6 +269,15 @@ int noc_lqr_params(int nx, int nu, int N, int B, const double* lam, const double
  * int32 (1 / 0; a NaN entry is infeasible).  One wave64 per trajectory. */
 int noc_check_feasibility(const noc_family* fam, int N, int B, const double* x, const double* u,
                           int* feasible, void* stream);
+
+/* The OCP's total_cost(x, u, bp) = final_cost(x_N) + sum_k stage_cost(x_k, u_k, bp)
+ * (examples/pendulum_runtime.py:53-56, examples/cartpole_runtime.py:48-51,
+ * examples/linear_demo_cuda.py:149-152; a registered family's own traced costs), evaluated where
+ * the reference's DDP evaluates it (noc/differential_dynamic_programming.py:108, 123-127).
+ * x (B, N+1, nx), u (B, N, nu), bp (B) barrier parameter per trajectory, cost (B).  One wave64
+ * per trajectory; an infeasible point's log barrier gives NaN, as jnp.log does. */
+int noc_total_cost(const noc_family* fam, int N, int B, const double* x, const double* u,
+                   const double* bp, double* cost, void* stream);
 
 /* Interior-point DDP (noc/differential_dynamic_programming.py: interior_point_ddp, D:189-208):
  * the whole barrier schedule of DDP iterations (second-order backward pass with the Vx . fxx

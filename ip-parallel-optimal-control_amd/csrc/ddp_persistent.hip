@@ -96,7 +96,8 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
   double bp = a.bp0;
   int total_it = 0, passes = 0;
   bool capped = false;
-  while (bp > 1e-4 && !capped) {  // ---------------- barrier schedule (D:189-208) ----------------
+  // ddp() at one barrier value (NOC_DDP_ONE_STAGE) runs whatever that value is (D:98-186)
+  while ((a.one_stage || bp > 1e-4) && !capped) {  // ------- barrier schedule (D:189-208) -------
     // rollout of the current controls (D:101, U:57-63): wave-uniform recurrence, lane 0 stores
     {
       double x[NX];

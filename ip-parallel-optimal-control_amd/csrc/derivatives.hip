@@ -145,6 +145,45 @@ hipError_t traj_feasibility(const noc_family& p, int N, int B, const double* x, 
   return hipErrorInvalidValue;
 }
 
+// total_cost(x, u, bp) = final_cost(x_N) + sum_k stage_cost(x_k, u_k, bp) (PR:53-56, CR:48-51,
+// LD:149-152; the OCP's own callable for a traced family).  One wave64 per trajectory, lanes
+// stride the stages, the wave's butterfly sum; bp per trajectory.
+template <int KIND, int NX, int NU>
+__global__ __launch_bounds__(64) void total_cost_kernel(noc_family prm, int N, int B,
+                                                        const double* x, const double* u,
+                                                        const double* bp, double* cost) {
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  Fam<KIND, NX, NU> f(prm);
+  const double bpb = bp[b];
+  double s = 0.0;
+  for (int k = threadIdx.x; k < N; k += 64) {
+    double xk[NX], uk[NU];
+    NOC_UNROLL for (int i = 0; i < NX; ++i) xk[i] = x[((size_t)b * (N + 1) + k) * NX + i];
+    NOC_UNROLL for (int j = 0; j < NU; ++j) uk[j] = u[((size_t)b * N + k) * NU + j];
+    s += f.stage_cost(xk, uk, bpb);
+  }
+  s = wave_sum(s);
+  if (threadIdx.x == 0) {
+    double xN[NX];
+    NOC_UNROLL for (int i = 0; i < NX; ++i) xN[i] = x[((size_t)b * (N + 1) + N) * NX + i];
+    cost[b] = f.final_cost(xN) + s;
+  }
+}
+
+hipError_t total_cost(const noc_family& p, int N, int B, const double* x, const double* u,
+                      const double* bp, double* cost, hipStream_t s) {
+#define NOC_FAMILY(K, X, U)                                                                    \
+  if (p.kind == K && p.nx == X && p.nu == U) {                                                 \
+    hipLaunchKernelGGL((total_cost_kernel<K, X, U>), dim3(B), dim3(64), 0, s, p, N, B, x, u, bp, \
+                       cost);                                                                  \
+    return hipGetLastError();                                                                  \
+  }
+#include NOC_FAMILIES_DEF
+#undef NOC_FAMILY
+  return hipErrorInvalidValue;
+}
+
 // ------------------------------------------------------------------------------------------------
 // costates lambda_k = cx_k + fx_k' lambda_{k+1} (C:43-54), lambda_N = lamT.
 // sequential (seq_costates, lax.scan): one thread per trajectory, the recurrence in stage order.

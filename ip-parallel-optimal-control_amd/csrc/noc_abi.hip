@@ -296,6 +296,20 @@ int noc_ipm_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* s
   return hip_status(noc::ipm_trial(*fam, *ws, mode, static_cast<hipStream_t>(stream)), "ipm_trial");
 }
 
+int noc_total_cost(const noc_family* fam, int N, int B, const double* x, const double* u,
+                   const double* bp, double* cost, void* stream) {
+  if (!fam) return fail(-2, "family is NULL");
+  if (!noc::family_supported(*fam)) return fail(-1, "unsupported problem family (kind/nx/nu)");
+  if (N < 1 || B < 0) return fail(-1, "need N >= 1, B >= 0");
+  int rc = 0;
+  if ((rc = check_ptr(x, "x", true, 8)) || (rc = check_ptr(u, "u", true, 8)) ||
+      (rc = check_ptr(bp, "bp", true, 8)) || (rc = check_ptr(cost, "cost", true, 8)))
+    return rc;
+  if (B == 0) return 0;
+  return hip_status(noc::total_cost(*fam, N, B, x, u, bp, cost, static_cast<hipStream_t>(stream)),
+                    "total_cost");
+}
+
 static int kkt_and_trial(const noc_family* fam, const noc_ipm_ws* ws, int mode, void* stream);
 
 int noc_ipm_step(const noc_family* fam, const noc_ipm_ws* ws, int mode, int terminal, int lanes,

@@ -141,6 +141,8 @@ hipError_t costates(int nx, int N, int B, const double* lamT, const double* cx, 
 hipError_t lqr_params(const LqrArgs& a, hipStream_t s);
 hipError_t traj_feasibility(const noc_family& p, int N, int B, const double* x, const double* u,
                             int* ok, hipStream_t s);
+hipError_t total_cost(const noc_family& p, int N, int B, const double* x, const double* u,
+                      const double* bp, double* cost, hipStream_t s);
 
 hipError_t kkt_dispatch(int nx, int nu, const KKTArgs& a, int lanes, hipStream_t stream);
 // lanes == 1: horizon-sequential solve, one trajectory per nx-lane group (kkt_group_impl.h)

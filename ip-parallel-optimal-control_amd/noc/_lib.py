@@ -25,7 +25,7 @@ KKT_KERNEL_SOURCES = {
     + _COMMON_SOURCES,
 }
 
-ABI_VERSION = 4  # include/noc_hip.h NOC_ABI_VERSION
+ABI_VERSION = 5  # include/noc_hip.h NOC_ABI_VERSION
 _dp = ctypes.c_void_p  # device pointers are passed as opaque addresses
 _i = ctypes.c_int
 
@@ -103,6 +103,7 @@ SIGNATURES.update({
     "noc_costates": (_i, [_i, _i, _i, _dp, _dp, _dp, _dp, _i, _dp]),
     "noc_lqr_params": (_i, [_i] * 4 + [_dp] * 13 + [_dp]),
     "noc_check_feasibility": (_i, [_fp, _i, _i, _dp, _dp, _dp, _dp]),
+    "noc_total_cost": (_i, [_fp, _i, _i, _dp, _dp, _dp, _dp, _dp]),
     "noc_ddp_work_doubles": (ctypes.c_longlong, [_i, _i, _i, _i]),
     "noc_ddp_supported": (_i, [_fp]),
     "noc_ddp_solve": (_i, [_fp, _i, _i] + [_dp] * 6 + [ctypes.c_double, _i, _dp]),

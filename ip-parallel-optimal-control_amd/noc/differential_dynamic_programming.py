@@ -8,7 +8,9 @@ own value gradient, so the recursion is horizon-sequential, not a scan; the stag
 evaluated lane-parallel).  Differences, all additive:
   * inputs may carry a leading batch axis (controls (B, N, nu), initial_state (B, nx)); the
     result is then batched too -- each trajectory follows its own reference control flow;
-  * `ocp.family` must be a registered family with nx <= 4 (noc.problems);
+  * `ocp.family` must be a registered family (noc.problems, noc.families); nx <= 4 runs the
+    one-launch kernel, larger states (nx = 8: the linear double-integrator stack) the same control
+    flow as a host loop over the device building blocks below (`_solve_blocks`);
   * return_info=True adds the backward-pass counts (incl. rejected retries) and final states.
 
 The module's building blocks keep the reference names too (D:10-186): compute_derivatives (the
@@ -26,7 +28,7 @@ import numpy as np
 from . import _lib
 from .optimal_control_problem import OCP, Derivatives
 from .par_interior_point_newton import (_dev, _family, check_traj_feasibility,
-                                        compute_derivatives, nonlin_rollout)
+                                        compute_derivatives, nonlin_rollout, total_cost)
 
 __all__ = ["compute_derivatives", "bwd_pass", "nonlin_rollout", "check_feasibility", "ddp",
            "interior_point_ddp"]
@@ -102,8 +104,10 @@ def _solve(ocp, controls, initial_state, device, bp0, max_passes, flags):
                             "kernels cannot evaluate Python callables")
     lib = _lib.load_for(ocp.family)
     fam = ocp.family.to_c()
-    if not lib.noc_ddp_supported(ctypes.byref(fam)):
-        raise _lib.NocError("interior-point DDP supports the registered families with nx <= 4")
+    blocks = not lib.noc_ddp_supported(ctypes.byref(fam))
+    if blocks and not (lib.noc_family_supported(ctypes.byref(fam))
+                       and _lib.for_shape(fam.nx, fam.nu).noc_kkt_supported(fam.nx, fam.nu) == 1):
+        raise _lib.NocError("interior-point DDP: family / shape not instantiated in this build")
     u = np.asarray(controls, dtype=np.float64)
     x0 = np.asarray(initial_state, dtype=np.float64)
     single = u.ndim == 2
@@ -117,6 +121,14 @@ def _solve(ocp, controls, initial_state, device, bp0, max_passes, flags):
     f64 = dict(device=dev, dtype=torch.float64)
     U = torch.as_tensor(np.ascontiguousarray(u), **f64)
     X0 = torch.as_tensor(np.ascontiguousarray(x0), **f64)
+    if blocks:
+        Xd, Ud, itd, passd, doned = _solve_blocks(ocp, U, X0, bp0, max_passes, flags)
+        X, Uh, itn = Xd.cpu().numpy(), Ud.cpu().numpy(), itd.to(torch.int32).cpu().numpy()
+        info = dict(passes=passd.to(torch.int32).cpu().numpy(), done=doned.cpu().numpy())
+        if single:
+            Uh, itn, X = Uh[0], int(itn[0]), X[0]
+            info = {k: v[0] for k, v in info.items()}
+        return X, Uh, itn, info
     work = torch.empty(int(lib.noc_ddp_work_doubles(nx, nu, N, Bt)), **f64)
     i32 = dict(device=dev, dtype=torch.int32)
     its, passes, done = (torch.zeros(Bt, **i32) for _ in range(3))
@@ -132,3 +144,79 @@ def _solve(ocp, controls, initial_state, device, bp0, max_passes, flags):
         Uh, itn, X = Uh[0], int(itn[0]), X[0]
         info = {k: v[0] for k, v in info.items()}
     return X, Uh, itn, info
+
+
+def _solve_blocks(ocp, U, X0, bp0, max_passes, flags):
+    """D:98-208 for the families the one-launch kernel does not instantiate (nx > 4: its lanes
+    hold the value Hessian and the stage blocks in registers): the same control flow, every
+    trajectory its own (masked updates), as a host loop over the device building blocks --
+    noc_derivatives, noc_ddp_bwd_pass, noc_nonlin_rollout, noc_check_feasibility, noc_total_cost.
+    One host synchronisation per retry (the loop conditions).  Returns final states, controls,
+    iterations, backward passes (retries included) and done (not stopped by max_passes), all on
+    the device."""
+    import torch
+    Bt, N, nu = U.shape
+    nx = X0.shape[-1]
+    dev = U.device
+    f64 = dict(dtype=torch.float64, device=dev)
+    i64 = dict(dtype=torch.int64, device=dev)
+
+    def sel(m, a, b):  # per-trajectory select
+        return torch.where(m.view(-1, *([1] * (a.dim() - 1))), a, b)
+
+    zK, zk = torch.zeros(Bt, N, nu, nx, **f64), torch.zeros(Bt, N, nu, **f64)
+    u = U.clone()
+    x = torch.zeros(Bt, N + 1, nx, **f64)
+    total_it, passes = torch.zeros(Bt, **i64), torch.zeros(Bt, **i64)
+    capped = torch.zeros(Bt, dtype=torch.bool, device=dev)
+    one_stage = bool(flags & _lib.DDP_ONE_STAGE)
+    inf = torch.full((Bt,), float("inf"), **f64)
+    bp = float(bp0)
+    while (one_stage or bp > 1e-4) and not bool(capped.all()):  # barrier schedule (D:189-208)
+        run = ~capped
+        nom = torch.zeros(Bt, N + 1, nx, **f64)
+        nom[:, 0] = X0
+        xr, _ = nonlin_rollout(ocp, zK, zk, nom, u)  # rollout of the controls (D:101): zero gains
+        x = sel(run, xr, x)
+        reg_param, reg_inc = torch.ones(Bt, **f64), torch.full((Bt,), 2.0, **f64)  # D:102-103
+        hu, it = torch.ones(Bt, **f64), torch.zeros(Bt, **i64)
+        active = run.clone()
+        while bool(active.any()):  # DDP iterations (D:105-170)
+            cost = total_cost(ocp, x, u, bp)  # D:108
+            d = compute_derivatives(ocp, x, u, bp)  # D:112
+            rp, r_inc = reg_param.clone(), reg_inc.clone()
+            inner = torch.zeros(Bt, **i64)
+            tx, tu, hn = x.clone(), u.clone(), hu.clone()
+            retry = active.clone()
+            while bool(retry.any()):  # retry loop (D:114-152)
+                k, K, pred, feas, Hu = bwd_pass(ocp, x[:, -1], d, rp)
+                xt, ut = nonlin_rollout(ocp, K, k, x, u)
+                new_cost = torch.where(check_traj_feasibility(ocp, xt, ut),
+                                       total_cost(ocp, xt, ut, bp), inf)  # D:121-125
+                gain = (new_cost - cost) / pred
+                succ = (gain > 0) & feas
+                rp_new = torch.where(succ, rp * torch.clamp(1.0 - (2.0 * gain - 1.0) ** 3,
+                                                            min=1.0 / 3.0),
+                                     rp * reg_inc)  # D:129-133: the outer reg_inc
+                r_inc_new = torch.where(succ, torch.full_like(r_inc, 2.0), 2.0 * r_inc)
+                rp = torch.where(retry, rp_new.clamp(1e-16, 1e16), rp)
+                r_inc = torch.where(retry, r_inc_new, r_inc)
+                tx, tu = sel(retry, xt, tx), sel(retry, ut, tu)
+                hn = torch.where(retry, Hu.abs().amax(dim=(1, 2)), hn)  # D:120
+                inner += retry.long()
+                passes += retry.long()
+                cap_now = retry & (passes >= max_passes)
+                capped |= cap_now
+                retry = retry & ~(succ | (inner > 500) | cap_now)
+            # the last trial becomes the nominal trajectory, accepted or not (D:154)
+            x, u = sel(active, tx, x), sel(active, tu, u)
+            reg_param = torch.where(active, rp, reg_param)
+            reg_inc = torch.where(active, r_inc, reg_inc)
+            hu = torch.where(active, hn, hu)
+            it += active.long()
+            active = active & ~((hu < 1e-4) | (it > 500) | capped)  # D:167-170
+        total_it += torch.where(run, it, torch.zeros_like(it))  # D:196
+        bp = bp / 5.0
+        if one_stage:
+            break
+    return x, u, total_it, passes, ~capped

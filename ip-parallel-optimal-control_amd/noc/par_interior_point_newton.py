@@ -119,6 +119,28 @@ def check_traj_feasibility(ocp: OCP, x, u):
     return ok[0] if single else ok
 
 
+def total_cost(ocp: OCP, states, controls, bp):
+    """ocp.total_cost(states, controls, bp) on the device (PR:53-56, CR:48-51, LD:149-152; a
+    registered family's own traced costs): final_cost(x_N) + sum_k stage_cost(x_k, u_k, bp)
+    (noc_total_cost, one wave per trajectory).  states (N+1, nx), controls (N, nu) -> a 0-d
+    tensor; batched -> (B,); bp a scalar or one per trajectory."""
+    fam = _family(ocp)
+    x, u = _dev(states, "states"), _dev(controls, "controls")
+    single = u.dim() == 2
+    if single:
+        x, u = x[None], u[None]
+    B, N = u.shape[0], u.shape[1]
+    if N == 0:
+        raise _lib.NocError("total_cost: need a horizon N >= 1")
+    bpt = torch.as_tensor(bp, dtype=torch.float64, device=u.device).reshape(-1).expand(B).contiguous()
+    cost = torch.empty(B, dtype=torch.float64, device=u.device)
+    lib = _lib.load_for(fam)
+    _lib.check(lib.noc_total_cost(ctypes.byref(fam.to_c()), N, B, x.data_ptr(), u.data_ptr(),
+                                  bpt.data_ptr(), cost.data_ptr(), _lib.stream_handle(u.device)),
+               "noc_total_cost", lib)
+    return cost[0] if single else cost
+
+
 def nonlin_rollout(ocp: OCP, gain, ffgain, nominal_states, nominal_controls):
     """P:87-104 (== D:73-90): x_hat_0 = x_0, u_hat = u + k + K (x_hat - x), x_hat+ =
     dynamics(x_hat, u_hat) -> (new_states (N+1, nx), new_controls (N, nu)); batched inputs

@@ -30,7 +30,7 @@ def test_library_exports_every_header_symbol():
     for f in header_functions():
         assert hasattr(lib, f), f
         assert f in _lib.SIGNATURES, f"ctypes mirror lacks {f}"
-    assert lib.noc_abi_version() == 4
+    assert lib.noc_abi_version() == 5
 
 
 def test_supported_shapes_and_lanes():

@@ -240,3 +240,90 @@ def test_ddp_one_stage_matches_oracle_and_chains_to_interior_point_ddp():
         bp = bp / 5
     Uf, itf = D.interior_point_ddp(ocp, u0, x0)
     assert np.array_equal(Uc, Uf) and np.array_equal(total, itf)
+
+
+@pytest.mark.gpu
+def test_ddp_nx8_building_block_loop_matches_oracle():
+    """nx = 8 (the constrained linear double-integrator stack, u box 5 with the log barrier): the
+    one-launch kernel is instantiated for nx <= 4, so interior_point_ddp runs the same control flow
+    as a host loop over the device building blocks (_solve_blocks).  Against the oracle's
+    interior_point_ddp: iterations within one, controls 1e-5, cost 1e-9; ddp() at one barrier
+    value too."""
+    from noc import differential_dynamic_programming as D
+    from noc import problems
+    from oracle import noc_oracle as O, problems as PR
+    N, Bt = 20, 2
+    rng = np.random.default_rng(41)
+    x0 = rng.normal(size=(Bt, 8))
+    u0 = 0.1 * rng.normal(size=(Bt, N, 4))
+    ocp = problems.double_integrators(4, 0.1, constrained=True)
+    U, its, info = D.interior_point_ddp(ocp, u0, x0, return_info=True)
+    assert info["done"].all() and (info["passes"] >= its).all()
+    prob = O.NumpyProblem(PR.linear_ocp(4, 0.1, constrained=True))
+    for b in range(Bt):
+        Ur, itr, _ = O.interior_point_ddp(prob, u0[b], x0[b])
+        assert abs(int(its[b]) - itr) <= 1, (b, int(its[b]), itr)
+        assert np.max(np.abs(U[b] - Ur)) < 1e-5, b
+        c = prob.total_cost(O.rollout(prob.dynamics, U[b], x0[b]), U[b], 0.8e-4)
+        cr = prob.total_cost(O.rollout(prob.dynamics, Ur, x0[b]), Ur, 0.8e-4)
+        assert abs(c - cr) <= 1e-9 * max(1.0, abs(cr)), b
+    X1, U1, it1 = D.ddp(ocp, u0, x0, 0.02)
+    for b in range(Bt):
+        Xr, Ur, itr, _ = O.ddp(prob, u0[b], x0[b], 0.02)
+        assert abs(int(it1[b]) - itr) <= 1
+        assert np.max(np.abs(U1[b] - Ur)) < 1e-5 and np.max(np.abs(X1[b] - Xr)) < 1e-5
+    # a max_passes cap stops the loop and says so
+    _, _, capped = D.interior_point_ddp(ocp, u0, x0, max_passes=2, return_info=True)
+    assert not capped["done"].any() and (capped["passes"] == 2).all()
+
+
+@pytest.mark.gpu
+def test_ddp_one_stage_below_the_schedule_floor():
+    """ddp(ocp, u, x0, bp) runs at any barrier value (D:98-186 has no bp test); the one-launch
+    kernel used to skip a bp <= 1e-4 as its schedule loop would."""
+    from noc import differential_dynamic_programming as D
+    from noc import problems
+    from oracle import noc_oracle as O
+    N = 20
+    ocp = problems.pendulum(1.0 / N)
+    x0, u0 = problems.initial_conditions("pendulum", N, 1, seed=5)
+    # warm start from the schedule's solution: a cold start at bp = 5e-5 runs ~150 non-convex
+    # iterations whose count rounding decides (see test_ddp_matches_oracle)
+    Uw, _ = D.interior_point_ddp(ocp, u0[0], x0[0])
+    X, U, its = D.ddp(ocp, Uw, x0[0], 5e-5)
+    Xr, Ur, itr, _ = O.ddp(_oracle_problem("pendulum", N), Uw, x0[0], 5e-5)
+    assert its >= 1 and abs(its - itr) <= 1, (its, itr)
+    assert np.max(np.abs(U - Ur)) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["pendulum", "cartpole", "linear8c"])
+def test_total_cost_matches_the_ocp_callable(name):
+    """noc_total_cost against the OCP's own host total_cost (PR:53-56, CR:48-51, LD:149-152), per
+    trajectory bp; an infeasible point's log barrier is NaN on both sides."""
+    import torch
+    from noc import problems
+    from noc.par_interior_point_newton import total_cost
+    N, Bt = 37, 3
+    if name == "linear8c":
+        ocp = problems.double_integrators(4, 0.1, constrained=True)
+        rng = np.random.default_rng(3)
+        x0, u = rng.normal(size=(Bt, 8)), 0.5 * rng.normal(size=(Bt, N, 4))
+    else:
+        ocp = problems.make_problem(name, N)
+        x0, u = problems.initial_conditions(name, N, Bt, seed=3)
+    X = np.zeros((Bt, N + 1, x0.shape[1]))
+    for b in range(Bt):
+        X[b, 0] = x0[b]
+        for k in range(N):
+            X[b, k + 1] = ocp.dynamics(X[b, k], u[b, k])
+    bp = np.array([0.1, 0.02, 1e-3])
+    got = total_cost(ocp, X, u, torch.tensor(bp, device="cuda")).cpu().numpy()
+    for b in range(Bt):
+        want = ocp.total_cost(X[b], u[b], bp[b])
+        assert abs(got[b] - want) <= 1e-12 * max(1.0, abs(want)), (b, got[b], want)
+    assert float(total_cost(ocp, X[0], u[0], bp[0])) == pytest.approx(got[0], rel=0, abs=0)
+    bad = u.copy()
+    bad[1, 5, 0] = 2 * ocp.family.u_bound
+    got = total_cost(ocp, X, bad, 0.1).cpu().numpy()
+    assert np.isfinite(got[0]) and np.isnan(got[1])
