@@ -400,3 +400,29 @@ def test_nx2_indefinite_state_cost(lanes):
         for k in ("dx", "du", "K", "d", "S", "v"):
             assert relerr(out[k][ok], ref[k][ok]) < RTOL, (k, relerr(out[k][ok], ref[k][ok]))
         assert relerr(out["pred"][ok], ref["pred"][ok]) < RTOL
+
+
+def test_kkt_random_shapes_match_oracle():
+    """Property form of the parity test (hypothesis, derandomized so every box draws the same 100
+    cases): any shape of the build, any horizon 1-260 (ragged chunks, N < lanes), any batch 1-9
+    (partly filled workgroups, the 512-register instance at one wave per SIMD), any lane count
+    incl. the batch-aware pick (0) and the group solve (1), affine terms on or off."""
+    from hypothesis import HealthCheck, given, settings, strategies as st
+
+    @settings(max_examples=100, deadline=None, derandomize=True, database=None,
+              suppress_health_check=list(HealthCheck))
+    @given(shape=st.sampled_from([(2, 1), (4, 1), (8, 4)]), N=st.integers(1, 260),
+           B=st.integers(1, 9), lanes=st.sampled_from([0, 1, 8, 16, 32, 64, 128]),
+           affine=st.booleans(), seed=st.integers(0, 2 ** 20))
+    def check(shape, N, B, lanes, affine, seed):
+        nx, nu = shape
+        if lanes == 128 and nx == 8:
+            lanes = 64
+        case = rand_lq(seed, B, N, nx, nu, affine=affine)
+        ref = oracle_batch(case)
+        out = run_kkt(case, lanes)
+        for k in ["dx", "du", "K", "d", "S", "v", "pred"]:
+            assert relerr(out[k], ref[k]) < RTOL, (k, shape, N, B, lanes, affine, seed)
+        assert np.array_equal(out["feasible"].astype(bool), ref["feasible"].astype(bool))
+
+    check()
