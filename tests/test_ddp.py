@@ -327,3 +327,65 @@ def test_total_cost_matches_the_ocp_callable(name):
     bad[1, 5, 0] = 2 * ocp.family.u_bound
     got = total_cost(ocp, X, bad, 0.1).cpu().numpy()
     assert np.isfinite(got[0]) and np.isnan(got[1])
+
+
+@pytest.mark.parametrize("one_stage", [False, True])
+def test_building_block_loop_control_flow_on_cpu(monkeypatch, one_stage):
+    """Host logic of the nx > 4 DDP path (_solve_blocks: masked per-trajectory control flow,
+    counters, the outer reg_inc quirk, the last-trial rule) on the CPU, with its device building
+    blocks replaced by the oracle's (test-only stand-ins): the loop must then reproduce the oracle's
+    interior_point_ddp / ddp exactly -- same iterations, same backward passes, same controls."""
+    import torch
+    from noc import _lib
+    from noc import differential_dynamic_programming as D
+    from noc.optimal_control_problem import Derivatives
+    from oracle import noc_oracle as O, problems as PR
+    N, Bt = 12, 3
+    prob = O.NumpyProblem(PR.pendulum_ocp(1.0 / N))
+    t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64))
+    npy = lambda a: a.detach().cpu().numpy()
+
+    def total_cost(ocp, x, u, bp):
+        return t([prob.total_cost(npy(x[b]), npy(u[b]), bp) for b in range(x.shape[0])])
+
+    def compute_derivatives(ocp, x, u, bp):
+        per = [prob.derivatives(npy(x[b]), npy(u[b]), bp) for b in range(x.shape[0])]
+        return Derivatives(*(t(np.stack([p[i] for p in per])) for i in range(10)))
+
+    def bwd_pass(ocp, xN, d, rp):
+        out = []
+        for b in range(xN.shape[0]):
+            Vx, Vxx = prob.final_grad_hess(npy(xN[b]))
+            out.append(O.ddp_bwd_pass(Vx, Vxx, tuple(npy(f[b]) for f in d), float(rp[b])))
+        k, K, pred, feas, Hu = zip(*out)
+        return t(np.stack(k)), t(np.stack(K)), t(pred), torch.tensor(feas), t(np.stack(Hu))
+
+    def nonlin_rollout(ocp, K, k, x, u):
+        out = [O.ddp_nonlin_rollout(prob, npy(K[b]), npy(k[b]), npy(x[b]), npy(u[b]))
+               for b in range(x.shape[0])]
+        return t(np.stack([o[0] for o in out])), t(np.stack([o[1] for o in out]))
+
+    def feasible(ocp, x, u):
+        return torch.tensor([prob.feasible(npy(x[b]), npy(u[b])) for b in range(x.shape[0])])
+
+    for name, fn in dict(total_cost=total_cost, compute_derivatives=compute_derivatives,
+                         bwd_pass=bwd_pass, nonlin_rollout=nonlin_rollout,
+                         check_traj_feasibility=feasible).items():
+        monkeypatch.setattr(D, name, fn)
+    rng = np.random.default_rng(17)
+    x0 = np.array([0.1, -0.1]) + 0.01 * rng.normal(size=(Bt, 2))
+    u0 = 0.1 * rng.normal(size=(Bt, N, 1))
+    flags = _lib.DDP_ONE_STAGE if one_stage else 0
+    X, U, its, passes, done = D._solve_blocks(None, t(u0), t(x0), 0.1, 10 ** 7, flags)
+    assert bool(done.all())
+    for b in range(Bt):
+        if one_stage:
+            Xr, Ur, itr, pr = O.ddp(prob, u0[b], x0[b], 0.1)
+            assert np.array_equal(npy(X[b]), Xr)
+        else:
+            Ur, itr, pr = O.interior_point_ddp(prob, u0[b], x0[b])
+        assert (int(its[b]), int(passes[b])) == (itr, pr), b
+        assert np.max(np.abs(npy(U[b]) - Ur)) <= 1e-12, b
+    # a cap of 5 backward passes stops every trajectory there and reports it
+    _, _, its5, passes5, done5 = D._solve_blocks(None, t(u0), t(x0), 0.1, 5, flags)
+    assert not bool(done5.any()) and bool((passes5 == 5).all())
