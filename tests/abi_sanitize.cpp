@@ -89,7 +89,26 @@ int main() {
   EXPECT(noc_ipm_solve(&fam, &ws, NOC_MODE_PAR, NOC_TERMINAL_STAGE0, 0.0, 10, 0) < 0);  // bp0
   EXPECT(noc_ipm_solve(&fam, &ws, NOC_MODE_PAR, NOC_TERMINAL_STAGE0, 0.1, 0, 0) < 0);   // cap
   EXPECT(noc_ipm_solve(nullptr, &ws, NOC_MODE_PAR, NOC_TERMINAL_STAGE0, 0.1, 10, 0) < 0);
+  // round-4 building blocks: NULL family / pointers, bad sizes, misaligned, unknown flags; an
+  // empty batch is a no-op
+  double* ph = p + 1;  // misaligned for doubles
+  EXPECT(noc_check_feasibility(nullptr, 10, 1, p, p, fe, 0) < 0);
+  EXPECT(noc_check_feasibility(&fam, 0, 1, p, p, fe, 0) < 0);
+  EXPECT(noc_check_feasibility(&fam, 10, 1, p, nullptr, fe, 0) < 0);
+  EXPECT(noc_check_feasibility(&fam, 10, 0, p, p, fe, 0) == 0);
+  EXPECT(noc_total_cost(nullptr, 10, 1, p, p, p, p, 0) < 0);
+  EXPECT(noc_total_cost(&fam, 10, -1, p, p, p, p, 0) < 0);
+  EXPECT(noc_total_cost(&fam, 10, 1, p, p, nullptr, p, 0) < 0);
+  EXPECT(noc_total_cost(&fam, 10, 1, p, p, p, ph, 0) < 0);
+  EXPECT(noc_total_cost(&fam, 10, 0, p, p, p, p, 0) == 0);
+  EXPECT(noc_nonlin_rollout(&fam, 10, 1, p, p, p, nullptr, p, p, 0) < 0);
+  EXPECT(noc_nonlin_rollout(&fam, 0, 1, p, p, p, p, p, p, 0) < 0);
+  EXPECT(noc_ddp_bwd_pass(3, 1, 10, 1, p, p, p, p, p, p, p, p, p, p, p, p, p, p, p, p, fe, p, 0) < 0);
+  EXPECT(noc_ddp_bwd_pass(4, 1, 10, 1, p, p, p, p, nullptr, p, p, p, p, p, p, p, p, p, p, p, fe, p, 0) < 0);
+  EXPECT(noc_ddp_solve_ex(&fam, 10, 1, p, p, p, fe, fe, fe, 0.1, 10, 2, 0) < 0);  // flag bit
+  EXPECT(noc_ddp_solve_ex(&fam, 10, 1, p, p, p, fe, fe, fe, 0.0, 10, 1, 0) < 0);  // bp0
   fam.nx = 3;
+  EXPECT(noc_total_cost(&fam, 10, 1, p, p, p, p, 0) < 0);  // family
   EXPECT(noc_ipm_prepare(&fam, &ws, NOC_MODE_PAR, NOC_TERMINAL_STAGE0, 0) < 0);  // family
   EXPECT(noc_ddp_work_doubles(0, 1, 10, 1) == -1 && noc_ddp_work_doubles(4, 1, 10, 2) > 0);
   EXPECT(noc_debug_phase_cycles(nullptr, 4, 0) < 0);
