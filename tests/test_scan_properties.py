@@ -18,12 +18,15 @@ from hypothesis import HealthCheck, given, settings, strategies as st
 import kernel_model as KM
 from lq_cases import rand_lq
 
-SETTINGS = settings(max_examples=30, deadline=None,
+SETTINGS = settings(max_examples=60, deadline=None, derandomize=True, database=None,
                     suppress_health_check=[HealthCheck.too_slow])
 
 
 @st.composite
 def shapes(draw, max_nx=4):
+    # any nu <= nx <= 4, and the c4 shapes nx = 8 with nu = 1 / 4
+    if draw(st.integers(0, 4)) == 0:
+        return draw(st.sampled_from([(8, 1), (8, 4)]))
     nx = draw(st.integers(1, max_nx))
     nu = draw(st.integers(1, nx))
     return nx, nu
