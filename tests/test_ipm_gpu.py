@@ -570,3 +570,42 @@ def test_cached_engine_gives_fresh_engine_results(mode, monkeypatch):
     nocache = [solve(ocp, u0[b], x0[b]) for b in range(2)]
     for (Uf, itf), (Un, itn) in zip(fresh, nocache):
         assert itf == itn and np.array_equal(Uf, Un)
+
+
+def test_random_solves_match_oracle():
+    """Property form of the solver parity tests (hypothesis, derandomized: every box draws the same
+    12 cases): pendulum or cart-pole, horizon 5-40, batch 1-2, par or seq, random initial states
+    and controls of the BASELINE distributions -- Newton iterations and (par) KKT solves equal to
+    the oracle's, controls within 1e-6, final cost within 1e-8."""
+    from hypothesis import HealthCheck, given, settings, strategies as st
+    from noc import problems
+    from noc.par_interior_point_newton import par_interior_point_optimal_control
+    from noc.seq_interior_point_newton import seq_interior_point_optimal_control
+    from oracle import noc_oracle as O
+
+    @settings(max_examples=12, deadline=None, derandomize=True, database=None,
+              suppress_health_check=list(HealthCheck))
+    @given(name=st.sampled_from(["pendulum", "cartpole"]), N=st.integers(5, 40),
+           B=st.integers(1, 2), par=st.booleans(), seed=st.integers(0, 2 ** 20))
+    def check(name, N, B, par, seed):
+        ocp = problems.make_problem(name, N)
+        x0, u0 = problems.initial_conditions(name, N, B, seed=seed)
+        prob = _oracle_problem(name, N)
+        if par:
+            U, its, info = par_interior_point_optimal_control(ocp, u0, x0, return_info=True)
+        else:
+            U, its = seq_interior_point_optimal_control(ocp, u0, x0)
+        for b in range(B):
+            if par:
+                Ur, itr, sr = O.par_interior_point_optimal_control(prob, u0[b], x0[b],
+                                                                   terminal="stage0")
+                assert info["kkt_solves"][b] == sr, (name, N, B, par, seed, b)
+            else:
+                Ur, itr = O.seq_interior_point_optimal_control(prob, u0[b], x0[b])
+            assert its[b] == itr, (name, N, B, par, seed, b, its[b], itr)
+            assert np.max(np.abs(U[b] - Ur)) < 1e-6
+            c = prob.total_cost(O.rollout(prob.dynamics, U[b], x0[b]), U[b], 0.0)
+            cr = prob.total_cost(O.rollout(prob.dynamics, Ur, x0[b]), Ur, 0.0)
+            assert abs(c - cr) <= 1e-8 * max(1.0, abs(cr))
+
+    check()
