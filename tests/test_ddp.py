@@ -389,3 +389,34 @@ def test_building_block_loop_control_flow_on_cpu(monkeypatch, one_stage):
     # a cap of 5 backward passes stops every trajectory there and reports it
     _, _, its5, passes5, done5 = D._solve_blocks(None, t(u0), t(x0), 0.1, 5, flags)
     assert not bool(done5.any()) and bool((passes5 == 5).all())
+
+
+@pytest.mark.gpu
+def test_random_ddp_solves_match_oracle():
+    """Property form of test_ddp_matches_oracle (hypothesis, derandomized: 8 cases): pendulum or
+    cart-pole, horizon 5-30, batch 1-2, random BASELINE-distribution starts -- iterations within
+    one of the oracle's (the documented rounding amplification), controls 1e-5, cost 1e-9."""
+    from hypothesis import HealthCheck, given, settings, strategies as st
+    from noc import problems
+    from noc.differential_dynamic_programming import interior_point_ddp
+    from oracle import noc_oracle as O
+
+    @settings(max_examples=8, deadline=None, derandomize=True, database=None,
+              suppress_health_check=list(HealthCheck))
+    @given(name=st.sampled_from(["pendulum", "cartpole"]), N=st.integers(5, 30),
+           B=st.integers(1, 2), seed=st.integers(0, 2 ** 20))
+    def check(name, N, B, seed):
+        ocp = problems.make_problem(name, N)
+        x0, u0 = problems.initial_conditions(name, N, B, seed=seed)
+        U, its, info = interior_point_ddp(ocp, u0, x0, return_info=True)
+        assert info["done"].all()
+        prob = _oracle_problem(name, N)
+        for b in range(B):
+            Ur, itr, _ = O.interior_point_ddp(prob, u0[b], x0[b])
+            assert abs(int(its[b]) - itr) <= 1, (name, N, B, seed, b, int(its[b]), itr)
+            assert np.max(np.abs(U[b] - Ur)) < 1e-5, (name, N, B, seed, b)
+            c = prob.total_cost(O.rollout(prob.dynamics, U[b], x0[b]), U[b], 0.8e-4)
+            cr = prob.total_cost(O.rollout(prob.dynamics, Ur, x0[b]), Ur, 0.8e-4)
+            assert abs(c - cr) <= 1e-9 * max(1.0, abs(cr)), (name, N, B, seed, b)
+
+    check()
