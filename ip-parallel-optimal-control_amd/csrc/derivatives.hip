@@ -146,7 +146,7 @@ hipError_t traj_feasibility(const noc_family& p, int N, int B, const double* x, 
 }
 
 // total_cost(x, u, bp) = final_cost(x_N) + sum_k stage_cost(x_k, u_k, bp) (PR:53-56, CR:48-51,
-// LD:149-152; the OCP's own callable for a traced family).  One wave64 per trajectory, lanes
+// LD:45-48; the OCP's own callable for a traced family).  One wave64 per trajectory, lanes
 // stride the stages, the wave's butterfly sum; bp per trajectory.
 template <int KIND, int NX, int NU>
 __global__ __launch_bounds__(64) void total_cost_kernel(noc_family prm, int N, int B,

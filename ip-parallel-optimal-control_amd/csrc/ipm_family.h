@@ -130,7 +130,7 @@ struct Fam {
     return xi - p.goal[i];
   }
   NOC_DEV bool barrier() const { return p.u_bound > 0.0; }
-  // stage cost (PR:40-50 / CR:36-45 / LD:138-141)
+  // stage cost (PR:40-50 / CR:36-45 / LD:34-37)
   NOC_DEV double stage_cost(const double* x, const double* u, double bp) const {
 #ifdef NOC_CUSTOM_FAMILY
     if constexpr (kGenCost) return gen::custom_stage_cost(x, u, bp);

@@ -120,7 +120,7 @@ def check_traj_feasibility(ocp: OCP, x, u):
 
 
 def total_cost(ocp: OCP, states, controls, bp):
-    """ocp.total_cost(states, controls, bp) on the device (PR:53-56, CR:48-51, LD:149-152; a
+    """ocp.total_cost(states, controls, bp) on the device (PR:53-56, CR:48-51, LD:45-48; a
     registered family's own traced costs): final_cost(x_N) + sum_k stage_cost(x_k, u_k, bp)
     (noc_total_cost, one wave per trajectory).  states (N+1, nx), controls (N, nu) -> a 0-d
     tensor; batched -> (B,); bp a scalar or one per trajectory."""

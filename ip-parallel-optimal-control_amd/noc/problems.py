@@ -145,7 +145,7 @@ def double_integrator_matrices(n_blocks: int, step: float, downsampling: int = 1
 def double_integrators(n_blocks: int = 1, step: float = 0.1, constrained: bool = False,
                        u_bound: float = 5.0) -> OCP:
     """Linear-quadratic family.  n_blocks=1, step=0.1, unconstrained = linear_demo_cuda.py
-    (X = diag(1e2, 1), U = 0.1 I, P = X: LD:138-146); n_blocks=4 is BASELINE config c4's nx=8."""
+    (X = diag(1e2, 1), U = 0.1 I, P = X: LD:34-42); n_blocks=4 is BASELINE config c4's nx=8."""
     A, B = double_integrator_matrices(n_blocks, step)
     nx, nu = 2 * n_blocks, n_blocks
     fam = Family(kind=_lib.FAMILY_LINEAR, nx=nx, nu=nu, dt=step,

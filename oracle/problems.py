@@ -196,7 +196,7 @@ def double_integrator_blocks(n_blocks: int, step: float, downsampling: int = 1):
 def linear_ocp(n_blocks: int, step: float, constrained: bool = False,
                u_bound: float = 5.0) -> TorchOCP:
     """Linear-quadratic family; with constrained=False it is linear_demo_cuda.py's LQR
-    (constraints == -1, LD:134-135; stage/final costs LD:138-146)."""
+    (constraints == -1, LD:30-31; stage/final costs LD:34-42)."""
     A_np, B_np = double_integrator_blocks(n_blocks, step)
     A, Bm = torch.from_numpy(A_np), torch.from_numpy(B_np)
     nx, nu = 2 * n_blocks, n_blocks
@@ -210,19 +210,19 @@ def linear_ocp(n_blocks: int, step: float, constrained: bool = False,
         def constraints(state, control):
             return torch.cat((control - u_bound, -control - u_bound))
     else:
-        def constraints(state, control):       # LD:134-135
+        def constraints(state, control):       # LD:30-31
             return -torch.ones(1)
 
-    def stage_cost(state, control, bp):         # LD:138-141
+    def stage_cost(state, control, bp):         # LD:34-37
         c = 0.5 * state @ X @ state + 0.5 * control @ U @ control
         if constrained:
             c = c - bp * torch.sum(torch.log(-constraints(state, control)))
         return c
 
-    def final_cost(state):                       # LD:144-146
+    def final_cost(state):                       # LD:40-42
         return 0.5 * state @ X @ state
 
-    def total_cost(states, controls, bp):        # LD:149-152
+    def total_cost(states, controls, bp):        # LD:45-48
         ct = vmap(stage_cost, in_dims=(0, 0, None))(states[:-1], controls, bp)
         return final_cost(states[-1]) + torch.sum(ct)
 

@@ -1,0 +1,96 @@
+"""Reference citations in the repo stay inside the files they cite.
+
+Every docstring, comment and document cites the reference as `<ABBR>:<line>[-<line>]` with the
+abbreviations of SURVEY.md (P = noc/par_interior_point_newton.py, ..., LD =
+examples/linear_demo_cuda.py).  A citation past the cited file's end is a wrong citation (round 4
+had LD:134-152, offset by the length of linear_mpc_parallel.py).  The line counts are pinned here so
+the test also runs where /root/reference is absent; where it is present they are re-checked, and so
+are a few anchor citations against the text they name.
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+
+FILES = {
+    "P": "noc/par_interior_point_newton.py",
+    "S": "noc/seq_interior_point_newton.py",
+    "C": "noc/costates.py",
+    "U": "noc/utils.py",
+    "T": "noc/optimal_control_problem.py",
+    "D": "noc/differential_dynamic_programming.py",
+    "PR": "examples/pendulum_runtime.py",
+    "CR": "examples/cartpole_runtime.py",
+    "LM": "examples/linear_mpc_parallel.py",
+    "LD": "examples/linear_demo_cuda.py",
+}
+# line counts (str.splitlines) of the reference files at the surveyed revision
+LINES = {"P": 254, "S": 202, "C": 54, "U": 63, "T": 30, "D": 208, "PR": 162, "CR": 174, "LM": 104,
+         "LD": 66}
+# the judge's and advisor's files quote wrong citations on purpose
+SKIP = {"VERDICT.md", "ADVICE.md"}
+CITE = re.compile(r"(?<![A-Za-z0-9_./])(PR|CR|LM|LD|P|S|C|U|T|D):(\d+)(?:-(\d+))?")
+# (abbr, first line, last line, text that must occur in that range)
+ANCHORS = [
+    ("LD", 19, 27, "def ode"),
+    ("LD", 30, 31, "def constraints"),
+    ("LD", 34, 37, "def stage_cost"),
+    ("LD", 40, 42, "def final_cost"),
+    ("LD", 45, 48, "def total_cost"),
+    ("P", 107, 124, "par_bwd_pass"),
+    ("P", 228, 254, "def par_interior_point_optimal_control"),
+    ("S", 42, 90, "def bwd_pass"),
+    ("C", 6, 12, "def combine_fc"),
+    ("U", 57, 63, "def rollout"),
+]
+
+
+def _tracked_text_files():
+    try:
+        out = subprocess.check_output(["git", "ls-files"], cwd=REPO, text=True)
+        files = out.split()
+    except (OSError, subprocess.CalledProcessError):
+        files = []
+        for root, _, names in os.walk(REPO):
+            if ".git" in root or "gpurun_out" in root:
+                continue
+            files += [os.path.relpath(os.path.join(root, n), REPO) for n in names]
+    keep = (".py", ".h", ".hip", ".md", ".c", ".cpp", ".def", ".sh")
+    return [f for f in files if f.endswith(keep) and os.path.basename(f) not in SKIP]
+
+
+def test_every_citation_is_inside_its_file():
+    bad, seen = [], 0
+    for rel in _tracked_text_files():
+        path = os.path.join(REPO, rel)
+        if not os.path.isfile(path):
+            continue
+        with open(path, encoding="utf-8", errors="replace") as fh:
+            for ln, line in enumerate(fh, 1):
+                for m in CITE.finditer(line):
+                    seen += 1
+                    a = int(m.group(2))
+                    b = int(m.group(3) or a)
+                    if not (1 <= a <= b <= LINES[m.group(1)]):
+                        bad.append(f"{rel}:{ln}: {m.group(0)} (file has {LINES[m.group(1)]} lines)")
+    assert seen > 500, seen  # the scan finds the repo's citations at all
+    assert not bad, "citations beyond the cited file:\n" + "\n".join(bad)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+def test_pinned_line_counts_match_the_reference():
+    for k, rel in FILES.items():
+        with open(os.path.join(REF, rel), encoding="utf-8") as fh:
+            assert len(fh.read().splitlines()) == LINES[k], rel
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("abbr,a,b,text", ANCHORS)
+def test_anchor_citations_name_the_right_code(abbr, a, b, text):
+    with open(os.path.join(REF, FILES[abbr]), encoding="utf-8") as fh:
+        lines = fh.read().splitlines()
+    assert text in "\n".join(lines[a - 1:b]), f"{abbr}:{a}-{b} does not contain {text!r}"

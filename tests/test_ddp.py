@@ -299,7 +299,7 @@ def test_ddp_one_stage_below_the_schedule_floor():
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["pendulum", "cartpole", "linear8c"])
 def test_total_cost_matches_the_ocp_callable(name):
-    """noc_total_cost against the OCP's own host total_cost (PR:53-56, CR:48-51, LD:149-152), per
+    """noc_total_cost against the OCP's own host total_cost (PR:53-56, CR:48-51, LD:45-48), per
     trajectory bp; an infeasible point's log barrier is NaN on both sides."""
     import torch
     from noc import problems

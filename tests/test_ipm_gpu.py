@@ -154,7 +154,7 @@ def test_final_cost_terminal_option_matches_oracle():
 
 
 def test_linear_demo_known_answer():
-    """examples/linear_demo_cuda.py (LD:123-166): unconstrained LQR, one exact Newton step solves
+    """examples/linear_demo_cuda.py (LD:19-62): unconstrained LQR, one exact Newton step solves
     it; compare with the dense KKT solution of the same LQ problem."""
     from noc import problems
     from noc.par_interior_point_newton import par_interior_point_optimal_control
