@@ -294,7 +294,10 @@ int noc_ddp_solve(const noc_family* fam, int N, int Bt, const double* x0, double
                   void* stream);
 /* noc_ddp_solve with flags: NOC_DDP_ONE_STAGE = ddp(ocp, controls, initial_state, barrier_param)
  * (noc/differential_dynamic_programming.py:98-186): the DDP iterations at bp0 only, no barrier
- * schedule; iterations[b] = that stage's DDP iterations, work starts with its final states. */
+ * schedule; iterations[b] = that stage's DDP iterations, work starts with its final states.
+ * bp0: any finite value >= 0 (the reference's ddp has no check on it, D:98; 0 = the unconstrained
+ * stage); the schedule (flags = 0) runs no stage for bp0 <= 1e-4 (D:194).  NaN, inf and negative
+ * values are rejected -- the same rule as the nx > 4 host loop of the Python module. */
 #define NOC_DDP_ONE_STAGE 1
 int noc_ddp_solve_ex(const noc_family* fam, int N, int Bt, const double* x0, double* u,
                      double* work, int* iterations, int* passes, int* done, double bp0,
@@ -306,7 +309,12 @@ int noc_ddp_solve_ex(const noc_family* fam, int N, int Bt, const double* x0, dou
  * noc_derivatives (natural layout, B leading); reg = reg_param[b] * ||cu_b||_F added to Quu.
  * Outputs ffgain k (B, N, nu), gain K (B, N, nu, nx), pred (B) = sum dV, feasible (B) int32 =
  * all eigh(Quu) > 0, Hu (B, N, nu) = Qu.  (nx, nu) as noc_kkt_supported; one thread per
- * trajectory (the recursion is nonlinear in V: no scan). */
+ * trajectory (the recursion is nonlinear in V: no scan).  Quu = cuu + fu'Vxx fu + Vx.fuu + reg I
+ * is READ AS SYMMETRIC: only its upper triangle is formed (cuu[i][j], fuu[m][i][j] with i <= j)
+ * and factorised LDL' (the pivots give the eigh > 0 test).  The reference (D:45-51) solves with
+ * the full Quu; the two agree whenever cuu and fuu are symmetric (Hessians) and Vxx is -- Vxx is
+ * propagated unsymmetrised as D:55 writes it, so a caller-supplied asymmetric Vxx or cuu / fuu
+ * gives k, K that differ from the reference by more than rounding. */
 int noc_ddp_bwd_pass(int nx, int nu, int N, int B, const double* Vx, const double* Vxx,
                      const double* reg_param, const double* cx, const double* cu,
                      const double* cxx, const double* cuu, const double* cxu, const double* fx,

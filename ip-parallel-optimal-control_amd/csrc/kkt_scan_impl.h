@@ -1037,12 +1037,17 @@ __global__ __launch_bounds__(L > 64 ? L : 256, (L > 64 || BIG) ? 1 : NOC_KKT_WAV
   if constexpr (L > 64 || BIG) asm volatile("" ::: "a255");
   const int traj = tid / L;
   if constexpr (L <= 64) {
-    // a wave with no trajectory to solve (past the batch, or masked off) still meets the one
+    // A wave with no trajectory to solve (past the batch, or masked off) still meets the one
     // workgroup barrier its block's other waves reach at the copy-out (lds_out, full / forward
-    // mode), so no wave of the block waits on a wave that has ended.  Uniform over the segment;
-    // two-wave segments (L = 128) are one trajectory per block, so their blocks return together.
-    if (traj >= a.B || (a.active && a.active[traj] == 0)) {
-      if (a.lds_out && a.mode != MODE_BWD) __syncthreads();
+    // mode, no early-exit ablation: the same condition as the main path's barrier), so every wave
+    // of the block issues that barrier exactly once.  With L < 64 one wave holds several
+    // segments, and only some may be dead: then the live segments' lanes issue the wave's one
+    // barrier at the copy-out and the dead lanes just leave -- the barrier here is taken only by
+    // a wave with no live segment at all (a wave-uniform branch, never lane-divergent).
+    const bool dead = traj >= a.B || (a.active && a.active[traj] == 0);
+    const bool wave_live = __any(!dead);  // voted at the wave's full EXEC, before any branch
+    if (dead) {
+      if (!wave_live && a.lds_out && a.mode != MODE_BWD && !(a.ablate & 6)) __syncthreads();
       return;
     }
   }

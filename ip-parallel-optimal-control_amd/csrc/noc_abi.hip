@@ -419,7 +419,10 @@ int noc_ddp_solve_ex(const noc_family* fam, int N, int Bt, const double* x0, dou
     return fail(-1, "DDP supports the registered families with nx <= 4 (noc_ddp_supported)");
   if (N < 1) return fail(-1, "horizon N must be >= 1");
   if (Bt < 0) return fail(-1, "batch Bt must be >= 0");
-  if (!(bp0 > 0.0)) return fail(-1, "bp0 must be > 0");
+  // any finite bp0 >= 0, like the reference ddp (D:98, no check on bp): bp0 = 0 is the
+  // unconstrained one-stage solve; the schedule (no NOC_DDP_ONE_STAGE) runs no stage for
+  // bp0 <= 1e-4, as interior_point_ddp's while loop (D:194) -- the same rule as the nx > 4 host loop
+  if (!(bp0 >= 0.0) || !(bp0 < INFINITY)) return fail(-1, "bp0 must be finite and >= 0");
   if (max_passes < 1) return fail(-1, "max_passes must be >= 1");
   int rc = 0;
   if ((rc = check_ptr(x0, "x0", true, 8)) || (rc = check_ptr(u, "u", true, 8)) ||

@@ -27,8 +27,9 @@ import numpy as np
 
 from . import _lib
 from .optimal_control_problem import OCP, Derivatives
-from .par_interior_point_newton import (_dev, _family, check_traj_feasibility,
-                                        compute_derivatives, nonlin_rollout, total_cost)
+from .par_interior_point_newton import (_dev, _expect_shapes, _family, _shape,
+                                        check_traj_feasibility, compute_derivatives,
+                                        nonlin_rollout, total_cost)
 
 __all__ = ["compute_derivatives", "bwd_pass", "nonlin_rollout", "check_feasibility", "ddp",
            "interior_point_ddp"]
@@ -53,15 +54,27 @@ def bwd_pass(final_cost, final_state, d: Derivatives, reg_param):
 
     class _O:  # noqa: N801 -- the family-bearing stand-in final_cost_grad expects
         family = fam
+    cus = _shape(d.cu)
+    single = len(cus) == 2
+    if len(cus) not in (2, 3):
+        raise _lib.NocError(f"bwd_pass: d.cu must be (N, nu) or (B, N, nu); got {cus}")
+    B, N = (1, cus[0]) if single else (cus[0], cus[1])
+    nx, nu = fam.nx, fam.nu
+    fields = dict(cx=(nx,), cu=(nu,), cxx=(nx, nx), cuu=(nu, nu), cxu=(nx, nu), fx=(nx, nx),
+                  fu=(nx, nu), fxx=(nx, nx, nx), fuu=(nx, nu, nu), fxu=(nx, nx, nu))
+    _expect_shapes("bwd_pass", single, B,
+                   [("final_state", final_state, (nx,))] +
+                   [(f"d.{f}", getattr(d, f), (N,) + fields[f]) for f in Derivatives._fields])
+    rps = _shape(reg_param)
+    if rps not in ((), (1,)) and rps != (B,):
+        raise _lib.NocError(f"bwd_pass: reg_param must be a scalar or one per trajectory ({B},); "
+                            f"got {rps}")
     xN = _dev(final_state, "final_state")
     dd = Derivatives(*(_dev(t) for t in d))
-    single = dd.cu.dim() == 2
     if single:
         xN = xN[None]
         dd = Derivatives(*(t[None] for t in dd))
     Vx, Vxx = final_cost_grad(_O, xN, hessian=True)
-    B, N, nu = dd.cu.shape
-    nx = dd.cx.shape[-1]
     dev = dd.cu.device
     f64 = dict(dtype=torch.float64, device=dev)
     rp = torch.as_tensor(reg_param, **f64).reshape(-1).expand(B).contiguous()
@@ -102,6 +115,8 @@ def _solve(ocp, controls, initial_state, device, bp0, max_passes, flags):
     if ocp.family is None:
         raise _lib.NocError("OCP has no registered device family (use noc.problems.*): the HIP "
                             "kernels cannot evaluate Python callables")
+    if not (np.isfinite(bp0) and bp0 >= 0.0):  # the rule of noc_ddp_solve_ex, for both paths
+        raise _lib.NocError(f"ddp: barrier parameter must be finite and >= 0, got {bp0}")
     lib = _lib.load_for(ocp.family)
     fam = ocp.family.to_c()
     blocks = not lib.noc_ddp_supported(ctypes.byref(fam))

@@ -20,6 +20,7 @@ Differences, all additive:
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import numpy as np
 import torch
@@ -43,6 +44,25 @@ def _dev(t, name="array"):
         _lib.require_device(t, name)
         return t.to(torch.float64).contiguous()
     return torch.as_tensor(np.ascontiguousarray(t, dtype=np.float64), device="cuda")
+
+
+def _shape(t):
+    return tuple(t.shape) if hasattr(t, "shape") else tuple(np.shape(t))
+
+
+def _expect_shapes(fn: str, single: bool, B, items):
+    """Raise NocError unless every (name, array, shape) of `items` has exactly `shape` (with the
+    leading batch axis B prepended when the call is batched).  Run on the host BEFORE any pointer
+    reaches a kernel: a mis-shaped input must raise, not make the device read or write out of
+    bounds (e.g. states without the terminal row, unbatched gains with batched states)."""
+    bad = []
+    for name, t, shp in items:
+        want = tuple(shp) if single else (B,) + tuple(shp)
+        got = _shape(t)
+        if got != want:
+            bad.append(f"{name} {got} (expected {want})")
+    if bad:
+        raise _lib.NocError(f"{fn}: mis-shaped input: " + "; ".join(bad))
 
 
 def compute_derivatives(ocp: OCP, states, controls, bp) -> Derivatives:
@@ -125,13 +145,18 @@ def total_cost(ocp: OCP, states, controls, bp):
     (noc_total_cost, one wave per trajectory).  states (N+1, nx), controls (N, nu) -> a 0-d
     tensor; batched -> (B,); bp a scalar or one per trajectory."""
     fam = _family(ocp)
-    x, u = _dev(states, "states"), _dev(controls, "controls")
-    single = u.dim() == 2
-    if single:
-        x, u = x[None], u[None]
-    B, N = u.shape[0], u.shape[1]
+    us = _shape(controls)
+    single = len(us) == 2
+    if len(us) not in (2, 3):
+        raise _lib.NocError(f"total_cost: controls must be (N, nu) or (B, N, nu); got {us}")
+    B, N = (1, us[0]) if single else (us[0], us[1])
+    _expect_shapes("total_cost", single, B, [("states", states, (N + 1, fam.nx)),
+                                             ("controls", controls, (N, fam.nu))])
     if N == 0:
         raise _lib.NocError("total_cost: need a horizon N >= 1")
+    x, u = _dev(states, "states"), _dev(controls, "controls")
+    if single:
+        x, u = x[None], u[None]
     bpt = torch.as_tensor(bp, dtype=torch.float64, device=u.device).reshape(-1).expand(B).contiguous()
     cost = torch.empty(B, dtype=torch.float64, device=u.device)
     lib = _lib.load_for(fam)
@@ -146,12 +171,20 @@ def nonlin_rollout(ocp: OCP, gain, ffgain, nominal_states, nominal_controls):
     dynamics(x_hat, u_hat) -> (new_states (N+1, nx), new_controls (N, nu)); batched inputs
     (leading B axis) give batched outputs (noc_nonlin_rollout, one thread per trajectory)."""
     fam = _family(ocp)
+    us = _shape(nominal_controls)
+    single = len(us) == 2
+    if len(us) not in (2, 3):
+        raise _lib.NocError(f"nonlin_rollout: nominal_controls must be (N, nu) or (B, N, nu); got {us}")
+    B, N = (1, us[0]) if single else (us[0], us[1])
+    nx, nu = fam.nx, fam.nu
+    _expect_shapes("nonlin_rollout", single, B, [("gain", gain, (N, nu, nx)),
+                                                 ("ffgain", ffgain, (N, nu)),
+                                                 ("nominal_states", nominal_states, (N + 1, nx)),
+                                                 ("nominal_controls", nominal_controls, (N, nu))])
     K, k = _dev(gain, "gain"), _dev(ffgain, "ffgain")
     x, u = _dev(nominal_states, "nominal_states"), _dev(nominal_controls, "nominal_controls")
-    single = u.dim() == 2
     if single:
         K, k, x, u = K[None], k[None], x[None], u[None]
-    B, N = u.shape[0], u.shape[1]
     xn, un = torch.empty_like(x), torch.empty_like(u)
     lib = _lib.load_for(fam)
     _lib.check(lib.noc_nonlin_rollout(ctypes.byref(fam.to_c()), N, B, K.data_ptr(), k.data_ptr(),
@@ -200,8 +233,11 @@ def par_Newton(nominal_states, d: Derivatives, reg_param, ru, Q, R, M):
 # at B = 1 over and over: the workspace allocation and its zero fill were part of every call's
 # host cost).  Every solve starts from the controls / initial state it loads -- the persistent
 # kernel and noc_ipm_init reset the whole solver state -- so a reused engine gives the results of
-# a fresh one.  Keyed by the family's descriptor bytes, so an edited family gets a new engine.
+# a fresh one.  Keyed by the family's descriptor bytes, so an edited family gets a new engine, and
+# by the calling thread, so cached engines are never shared across threads (the cache dict itself
+# is guarded by a lock).
 _ENGINES: "dict" = {}
+_ENGINES_LOCK = threading.Lock()
 _ENGINE_CACHE_MAX = 8
 _ENGINE_CACHE_STAGES = 1 << 16  # Bt * N at most: B = 1 up to N = 65536, B = 64 at N = 1000
 
@@ -212,15 +248,19 @@ def _engine(fam, N, Bt, lanes, device):
     persistent = lanes in (0, 64) and persistent_supported(fam, N)
     if Bt * N > _ENGINE_CACHE_STAGES:
         return BatchedIPM(fam, N, Bt, device=device, lanes=lanes, persistent=persistent)
+    # per thread: an engine is a workspace, so two threads solving the same shape must not share
+    # one (the reference's functions have no shared state)
     key = (id(fam), bytes(fam.to_c()), getattr(fam, "lib_path", None), N, Bt, lanes, persistent,
-           str(torch.device(device)))
-    eng = _ENGINES.pop(key, None)
+           str(torch.device(device)), threading.get_ident())
+    with _ENGINES_LOCK:
+        eng = _ENGINES.pop(key, None)
     if eng is None:
         eng = BatchedIPM(fam, N, Bt, device=device, lanes=lanes, persistent=persistent)
         eng._family_ref = fam  # keeps id(fam) from being reused while the entry lives
-    _ENGINES[key] = eng  # most recently used last
-    while len(_ENGINES) > _ENGINE_CACHE_MAX:
-        _ENGINES.pop(next(iter(_ENGINES)))
+    with _ENGINES_LOCK:
+        _ENGINES[key] = eng  # most recently used last
+        while len(_ENGINES) > _ENGINE_CACHE_MAX:
+            _ENGINES.pop(next(iter(_ENGINES)))
     return eng
 
 

@@ -4,6 +4,7 @@
 // before a kernel launch, or fails cleanly at the launch when no device is visible).  Checks that
 // each invalid argument returns a negative status with a message, never touches memory it must
 // not, and that the queries stay in range.
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -106,7 +107,8 @@ int main() {
   EXPECT(noc_ddp_bwd_pass(3, 1, 10, 1, p, p, p, p, p, p, p, p, p, p, p, p, p, p, p, p, fe, p, 0) < 0);
   EXPECT(noc_ddp_bwd_pass(4, 1, 10, 1, p, p, p, p, nullptr, p, p, p, p, p, p, p, p, p, p, p, fe, p, 0) < 0);
   EXPECT(noc_ddp_solve_ex(&fam, 10, 1, p, p, p, fe, fe, fe, 0.1, 10, 2, 0) < 0);  // flag bit
-  EXPECT(noc_ddp_solve_ex(&fam, 10, 1, p, p, p, fe, fe, fe, 0.0, 10, 1, 0) < 0);  // bp0
+  EXPECT(noc_ddp_solve_ex(&fam, 10, 1, p, p, p, fe, fe, fe, -1.0, 10, 1, 0) < 0);  // bp0 < 0
+  EXPECT(noc_ddp_solve_ex(&fam, 10, 1, p, p, p, fe, fe, fe, NAN, 10, 1, 0) < 0);  // bp0 NaN
   fam.nx = 3;
   EXPECT(noc_total_cost(&fam, 10, 1, p, p, p, p, 0) < 0);  // family
   EXPECT(noc_ipm_prepare(&fam, &ws, NOC_MODE_PAR, NOC_TERMINAL_STAGE0, 0) < 0);  // family

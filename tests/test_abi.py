@@ -188,7 +188,9 @@ def test_ddp_queries_and_argument_errors_without_gpu():
     args = [16, 16, 16, 16, 16, 16]  # 16-byte aligned fake device addresses: never dereferenced
     assert lib.noc_ddp_solve(None, 10, 1, *args, 0.1, 10, None) == -2
     assert lib.noc_ddp_solve(ctypes.byref(pend), 0, 1, *args, 0.1, 10, None) < 0
-    assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 1, *args, 0.0, 10, None) < 0
+    assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 1, *args, -0.5, 10, None) < 0
+    assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 1, *args, float("nan"), 10, None) < 0
+    assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 1, *args, float("inf"), 10, None) < 0
     assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 1, *args, 0.1, 0, None) < 0
     assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 1, None, *args[1:], 0.1, 10, None) == -2
     assert lib.noc_ddp_solve(ctypes.byref(pend), 10, 0, *args, 0.1, 10, None) == 0  # empty batch

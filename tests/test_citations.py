@@ -3,7 +3,7 @@
 Every docstring, comment and document cites the reference as `<ABBR>:<line>[-<line>]` with the
 abbreviations of SURVEY.md (P = noc/par_interior_point_newton.py, ..., LD =
 examples/linear_demo_cuda.py).  A citation past the cited file's end is a wrong citation (round 4
-had LD:134-152, offset by the length of linear_mpc_parallel.py).  The line counts are pinned here so
+had linear_demo_cuda.py citations offset by the 104 lines of linear_mpc_parallel.py).  The line counts are pinned here so
 the test also runs where /root/reference is absent; where it is present they are re-checked, and so
 are a few anchor citations against the text they name.
 """
