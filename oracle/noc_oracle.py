@@ -31,6 +31,14 @@ import numpy as np
 # ----------------------------------------------------------------------------------------------
 
 
+
+def _cube(c):
+    """(2 gain - 1) ** 3 of S:141 / P:169 / D:131 as JAX evaluates it: `x ** 3` with a Python int
+    is lax.integer_pow, lowered by repeated squaring to x * (x * x) -- two roundings, which can
+    differ from numpy's pow(x, 3.0) in the last bit (and the device kernels multiply the same
+    way).  A last-bit difference in rp steers every later step."""
+    return c * (c * c)
+
 def rollout(dynamics, controls: np.ndarray, x0: np.ndarray) -> np.ndarray:
     """U:57-63 -- sequential x_{k+1} = f(x_k, u_k); returns (N+1, nx)."""
     xs = [np.asarray(x0, dtype=np.float64)]
@@ -336,7 +344,7 @@ def seq_newton_oc(prob, U, x0, bp, max_iter=100000):
             gain = (new_cost - cost) / pred
         accept = bool(gain > 0) and bpf
         if accept:
-            mu = mu * max(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) ** 3)
+            mu = mu * max(1.0 / 3.0, 1.0 - _cube(2.0 * gain - 1.0))
             nu_ = 2.0
             X, U = tX, tU
         else:
@@ -387,7 +395,7 @@ def par_newton_oc(prob, U, x0, bp, terminal="final_cost", trace=None):
                 gain = (new_cost - cost) / pred
             success = bool(gain > 0.0) and feas
             if success:
-                rp = rp * max(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) ** 3)
+                rp = rp * max(1.0 / 3.0, 1.0 - _cube(2.0 * gain - 1.0))
                 r_inc = 2.0
             else:
                 rp = rp * r_inc
@@ -488,7 +496,7 @@ def ddp(prob, U, x0, bp, trace=None):
                 gain = (new_cost - cost) / pred
             success = bool(gain > 0) and feas                          # D:128
             if success:
-                rp = rp * max(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) ** 3)
+                rp = rp * max(1.0 / 3.0, 1.0 - _cube(2.0 * gain - 1.0))
                 r_inc = 2.0
             else:
                 rp = rp * reg_inc                                       # outer reg_inc (D:132)
@@ -496,7 +504,8 @@ def ddp(prob, U, x0, bp, trace=None):
             rp = min(max(rp, 1e-16), 1e16)                              # D:135
             inner += 1
             if trace is not None:
-                trace.append(dict(it=it, inner=inner, pred=pred, gain=gain, success=success, rp=rp))
+                trace.append(dict(it=it, inner=inner, pred=pred, gain=gain, success=success, rp=rp,
+                                  cost=cost, new_cost=new_cost, hu=Hn))
             if success or inner > 500:                                  # D:147-152
                 break
         X, U, Hu_norm, reg_param, reg_inc = TX, TU, Hn, rp, r_inc       # D:154-162
