@@ -71,6 +71,9 @@ struct StageData {
   Vec<NX> c;
 };
 
+typedef __attribute__((address_space(3))) double lds_double;
+typedef __attribute__((address_space(3))) noc_dbl2 lds_dbl2;
+
 template <int NX>
 struct Elem {
   Mat<NX, NX> A;
@@ -81,13 +84,14 @@ struct Elem {
 };
 
 // PART: 0 = the whole stage, 1 = everything but Q, 2 = Q only (phase 3 prefetches part 1 of the
-// next stage and loads Q, which the Riccati step uses last, at the top of the current one)
+// next stage and loads Q, which the Riccati step uses last, at the top of the current one),
+// 3 = everything but A, B (the scan instances that keep A, B on chip: kkt_scan_wave_src, AB)
 template <int NX, int NU, int L, bool AFF, bool TILED, int PART = 0>
 NOC_DEV void load_stage(const KKTArgs& a, int traj, size_t si, int j, int l, int cmax, double reg,
                         StageData<NX, NU>& st) {
-  constexpr bool REST = PART != 2, WQ = PART != 1;
+  constexpr bool REST = PART != 2, WQ = PART != 1, WAB = REST && PART != 3;
   if constexpr (TILED) {
-    if constexpr (REST) {
+    if constexpr (WAB) {
       tload<NX * NX, L>(a.A, traj, j, l, cmax, st.A.v);
       tload<NX * NU, L>(a.Bm, traj, j, l, cmax, st.B.v);
     }
@@ -102,7 +106,7 @@ NOC_DEV void load_stage(const KKTArgs& a, int traj, size_t si, int j, int l, int
       }
     }
   } else {
-    if constexpr (REST) {
+    if constexpr (WAB) {
       gload<NX * NX>(a.A + si * (NX * NX), st.A.v);
       gload<NX * NU>(a.Bm + si * (NX * NU), st.B.v);
     }
@@ -420,7 +424,7 @@ NOC_DEV void rev_scan_sklansky(Elem<NX>& e) {
 // On-chip slot region of one trajectory (one per L-lane segment of the workgroup): N slots
 // of KD = NU*(NX+1) doubles (K_s, d_s after phase 3, then x_s, u_s in phase 4) + x_N.
 template <int NX, int NU>
-NOC_DEV constexpr int kd_width() { return NU * (NX + 1); }
+__host__ __device__ constexpr int kd_width() { return NU * (NX + 1); }
 template <int NX, int NU, int L>
 NOC_DEV double* lds_slots(int N) {
   extern __shared__ __attribute__((aligned(16))) double noc_smem[];
@@ -436,6 +440,53 @@ template <int NX, int NU>
 NOC_DEV double* lds_join(int N, bool slots_staged) {
   extern __shared__ __attribute__((aligned(16))) double noc_smem[];
   return noc_smem + (slots_staged ? ((N * kd_width<NX, NU>() + NX + 1) & ~1) : 0);
+}
+
+// A, B slots of the instances that own a SIMD (AB; a.ab_slots > 0): phase 1 parks each stage's A,
+// B of chunk slots j < a.ab_slots in LDS, phases 3 and 4 read them back from there instead of
+// re-reading them from the memory-side cache.  Behind the block's K, d slot regions (and the
+// two-wave join region), one region per wave: [slot j][16-byte granule g][lane] -- every access a
+// conflict-free ds_read / ds_write_b128 of the lane's own granule.
+template <int NX, int NU>
+__host__ __device__ constexpr int ab_granules() { return (NX * NX + NX * NU) / 2; }
+template <int NX, int NU>
+__host__ __device__ constexpr bool ab_supported() { return (NX * NX) % 2 == 0 && (NX * NU) % 2 == 0; }
+template <int NX, int NU>
+NOC_DEV lds_double* lds_ab(int lds_base, int ab_slots) {
+  extern __shared__ __attribute__((aligned(16))) double noc_smem[];
+  return (lds_double*)(noc_smem + lds_base + (size_t)(threadIdx.x / 64) * ab_slots * ab_granules<NX, NU>() * 128 +
+                      2 * (threadIdx.x & 63));
+}
+
+template <int NX, int NU>
+NOC_DEV void ab_store(lds_double* lab, int j, const Mat<NX, NX>& A, const Mat<NX, NU>& Bm) {
+  lds_double* p = lab + j * ab_granules<NX, NU>() * 128;
+  NOC_UNROLL for (int q = 0; q < NX * NX / 2; ++q) {
+    noc_dbl2 v;
+    v.x = A.v[2 * q];
+    v.y = A.v[2 * q + 1];
+    *reinterpret_cast<lds_dbl2*>(p + q * 128) = v;
+  }
+  NOC_UNROLL for (int q = 0; q < NX * NU / 2; ++q) {
+    noc_dbl2 v;
+    v.x = Bm.v[2 * q];
+    v.y = Bm.v[2 * q + 1];
+    *reinterpret_cast<lds_dbl2*>(p + (NX * NX / 2 + q) * 128) = v;
+  }
+}
+template <int NX, int NU>
+NOC_DEV void ab_load(const lds_double* lab, int j, Mat<NX, NX>& A, Mat<NX, NU>& Bm) {
+  const lds_double* p = lab + j * ab_granules<NX, NU>() * 128;
+  NOC_UNROLL for (int q = 0; q < NX * NX / 2; ++q) {
+    const noc_dbl2 v = *reinterpret_cast<const lds_dbl2*>(p + q * 128);
+    A.v[2 * q] = v.x;
+    A.v[2 * q + 1] = v.y;
+  }
+  NOC_UNROLL for (int q = 0; q < NX * NU / 2; ++q) {
+    const noc_dbl2 v = *reinterpret_cast<const lds_dbl2*>(p + (NX * NX / 2 + q) * 128);
+    Bm.v[2 * q] = v.x;
+    Bm.v[2 * q + 1] = v.y;
+  }
 }
 
 // e1 <- e1 (x) (value-only e2 = (J2, nu2)): the true value function at e1's start given the value
@@ -506,6 +557,10 @@ struct ArgsSrc {
   NOC_DEV void ab(int s, int j, Mat<NX, NX>& A, Mat<NX, NU>& Bm, Vec<NX>& c) const {
     load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + s, j, l, cmax, A, Bm, c);
   }
+  NOC_DEV void cvec(int s, int j, Vec<NX>& c) const {  // the affine term alone (a.c set)
+    if constexpr (TILED) tload<NX, L>(a.c, traj, j, l, cmax, c.v);
+    else gload<NX>(a.c + (tN + s) * NX, c.v);
+  }
 };
 
 // The whole KKT solve of trajectory `traj` by lane `l` of its L-lane segment (the kernel below;
@@ -519,8 +574,12 @@ struct ArgsSrc {
 // scan: −1 stage of phase 4's re-reads); off inside the persistent solver, whose register budget
 // it would push into scratch (444 -> 516 B/lane).
 // BIG: the instance owns a SIMD (512 registers): the combines run masked (no identity partner).
+// AB (default: the 512-register L = 32 / 64 instances, BIG, where one wave per SIMD leaves 40 KB of
+// LDS per wave): A, B of chunk slots j < a.ab_slots stay in LDS from phase 1 to phases 3 and 4
+// (lds_ab); a.ab_slots = 0 turns it off at run time.  Not in the two-wave segments (L = 128): their
+// re-reads are L2 hits already, and the slots measured +2.5 % there (profiles/r05/ab_slots/).
 template <int NX, int NU, int L, bool AFF, bool TILED, class SRC, int CACHE = 0, bool HANDOFF = true,
-          bool BIG = false>
+          bool BIG = false, bool AB = (BIG && ab_supported<NX, NU>())>
 NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, const SRC& src) {
   constexpr int KD = kd_width<NX, NU>();
   if (traj >= a.B) return;                     // uniform over the segment
@@ -545,6 +604,14 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   (void)wv;
   (void)lw;
   (void)join;
+  lds_double* lab = nullptr;
+  int abn = 0;  // chunk slots whose A, B are parked in LDS
+  if constexpr (AB) {
+    // (MODE_FWD has no phase 1 to park them; ablation bit 4 reads other trajectories' blocks;
+    // ablation bit 6 turns the slots off -- results identical, tests/test_kkt_gpu.py)
+    abn = (CACHE == 0 && a.mode != MODE_FWD && !(a.ablate & (16 | 64))) ? a.ab_slots : 0;
+    if (abn > 0) lab = lds_ab<NX, NU>(a.lds_base, a.ab_slots);
+  }
   NOC_STAMP(0);
   StageData<NX, NU> cache[CACHE > 0 ? CACHE : 1];
   if constexpr (CACHE > 0) {
@@ -589,6 +656,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       for (int s = start + len - 1; s >= start; --s) {
         StageData<NX, NU> st;
         src.stage(s, s - start, reg, st);
+        if constexpr (AB) { if (s - start < abn) ab_store<NX, NU>(lab, s - start, st.A, st.B); }
         prepend<NX, NU, AFF>(e, st, reg);
       }
     }
@@ -650,6 +718,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     double pred = 0.0;
     int feas = 1;
     double* skd = lds_slots<NX, NU, L>(N);  // K, d stay on chip for phase 4 when staged
+    auto stage3 = [&](int s, StageData<NX, NU>& st) { src_re.stage(s, s - start, reg, st); };
     auto riccati_stage = [&](const int s, const StageData<NX, NU>& st) {
       Mat<NX, NX> SA;
       Mat<NX, NU> SB;
@@ -763,15 +832,34 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       // not software pipelined: prefetching stage s-1 during stage s (registers) was measured
       // slower (phase 3 44k -> 60k cycles per wave at c3: the prefetch spills, and the phase runs
       // at the memory-side-cache rate, not at a per-stage latency, tools/scan_stamps.py)
-      if constexpr (HANDOFF) {
+      bool split = false;
+      if constexpr (AB) split = abn > 0;
+      if (split) {
+        // AB: the chunk's slots j >= abn re-read whole, then j < abn with A, B from LDS -- two
+        // branch-free loops; no hand-off (phase 4 reads slot 0's A, B from LDS as well)
+        if constexpr (AB) {
+          const int jl = len < abn ? len : abn;
+          for (int s = start + len - 1; s >= start + jl; --s) {
+            StageData<NX, NU> st;
+            src_re.stage(s, s - start, reg, st);
+            riccati_stage(s, st);
+          }
+          for (int s = start + jl - 1; s >= start; --s) {
+            StageData<NX, NU> st;
+            src_re.template stage_part<3>(s, s - start, reg, st);
+            ab_load<NX, NU>(lab, s - start, st.A, st.B);
+            riccati_stage(s, st);
+          }
+        }
+      } else if constexpr (HANDOFF) {
         for (int s = start + len - 1; s > start; --s) {
           StageData<NX, NU> st;
-          src_re.stage(s, s - start, reg, st);
+          stage3(s, st);
           riccati_stage(s, st);
         }
         if (len > 0) {  // the chunk's first stage, peeled: its A, B (c) go on to phase 4
           StageData<NX, NU> st;
-          src_re.stage(start, 0, reg, st);
+          stage3(start, st);
           riccati_stage(start, st);
           hA = st.A;
           hB = st.B;
@@ -781,7 +869,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       } else {
         for (int s = start + len - 1; s >= start; --s) {
           StageData<NX, NU> st;
-          src_re.stage(s, s - start, reg, st);
+          stage3(s, st);
           riccati_stage(s, st);
         }
       }
@@ -945,10 +1033,33 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       }
     }
   } else {
+    // AB: the chunk's first slots with A, B from LDS (no prefetch needed), then the rest as below
+    int s0 = start;
+    if constexpr (AB) {
+      if (abn > 0) {
+        const int jl = len < abn ? len : abn;
+        for (int s = start; s < start + jl; ++s) {
+          Mat<NX, NX> A;
+          Mat<NX, NU> Bm;
+          Vec<NX> cc;
+          ab_load<NX, NU>(lab, s - start, A, Bm);
+          set_zero(cc);
+          if constexpr (AFF) { if (a.c) src_re.cvec(s, s - start, cc); }
+          double Kk[NU * (NX + 1)];
+          if (kd_lds) {
+            NOC_UNROLL for (int i = 0; i < NU * (NX + 1); ++i) Kk[i] = slot[s * KD + i];
+          } else {
+            load_Kd<NX, NU, L, TILED>(a, traj, tN + s, s - start, l, cmax, Kk);
+          }
+          fwd_stage(s, A, Bm, cc, Kk);
+        }
+        s0 = start + jl;
+      }
+    }
     // one stage prefetched (a two-deep prefetch measured no faster: the propagation runs at the
     // rate the A, B re-reads stream at, not at the per-stage latency)
-    if (len > 0) {
-      if (handed) {  // stage `start` from phase 3's registers; only its K, d from the LDS slot
+    if (s0 < start + len) {
+      if (handed && s0 == start) {  // stage `start` from phase 3's registers; only its K, d from LDS
         nA = hA;
         nB = hB;
         nc = hc;
@@ -958,10 +1069,10 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
           load_Kd<NX, NU, L, TILED>(a, traj, tN + start, 0, l, cmax, nK);
         }
       } else {
-        fetch(start);
+        fetch(s0);
       }
     }
-    for (int s = start; s < start + len; ++s) {
+    for (int s = s0; s < start + len; ++s) {
       const Mat<NX, NX> A = nA;
       const Mat<NX, NU> Bm = nB;
       const Vec<NX> cc = nc;
@@ -1067,22 +1178,47 @@ template <int NX, int NU, int L, bool AFF>
 hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
   KKTArgs a = a_in;
   const long long threads = (long long)a.B * L;
-  // L <= 64: wpb independent waves per workgroup (no LDS sharing; each its own slot region);
-  // L = 128: one trajectory per two-wave workgroup (the waves join through LDS)
-  const size_t slots1 = (a.mode == MODE_BWD || (!a.dx && !a.du)) ? 0 : kkt_lds_bytes_rt(NX, NU, a.N, L);
-  const int wpb = L > 64 ? 1 : kkt_waves_per_block((threads + 63) / 64, slots1);
-  const int block = L > 64 ? L : 64 * wpb;
-  const unsigned grid = (unsigned)((threads + block - 1) / block);
-  const size_t slots = slots1 * wpb;
-  a.lds_out = slots > 0 ? 1 : 0;
-  const size_t lds = slots + (L > 64 ? join_doubles<NX>() * sizeof(double) : 0);
-  if (!a.lds_out && (!a.K || !a.d)) return hipErrorInvalidValue;  // K/d needed as workspace
   constexpr int CC = kkt_cache_len<NX, NU, L>();
   const int cmax = a.N / L + (a.N % L ? 1 : 0);
   const bool cached = CC > 0 && cmax <= CC && !(a.ablate & 8);  // ablation bit 3: streamed chunks
   // the batch's waves fit one per SIMD: the 512-register instance (NOC_KKT_BIG=0 disables)
   const bool big = (L == 64 || L == 32) && NX >= 3 && NX <= 4 &&
                    (threads + 63) / 64 <= kkt_device_simds() && kkt_big_enabled();
+  // L <= 64: wpb independent waves per workgroup (no LDS sharing; each its own slot region);
+  // L = 128: one trajectory per two-wave workgroup (the waves join through LDS)
+  const size_t slots1 = (a.mode == MODE_BWD || (!a.dx && !a.du)) ? 0 : kkt_lds_bytes_rt(NX, NU, a.N, L);
+  int wpb = L > 64 ? 1 : kkt_waves_per_block((threads + 63) / 64, slots1);
+  size_t lds = slots1 * wpb + (L > 64 ? join_doubles<NX>() * sizeof(double) : 0);
+  a.lds_out = slots1 > 0 ? 1 : 0;
+  a.ab_slots = 0;
+  a.lds_base = 0;
+  // The 512-register instances (BIG) have 40 KB of LDS per wave (160 KB per CU at one wave per
+  // SIMD) against the slots' <= 20 KB: behind the slots they keep A, B of as many chunk slots as
+  // fit (AB), one wave per workgroup
+  if (big) {
+    const size_t per_traj = (size_t)(((long long)a.N * kd_width<NX, NU>() + NX + 1) & ~1LL);
+    const size_t segs = 64 / L;
+    const size_t base = slots1 > 0 ? segs * per_traj : 0;
+    const size_t waves = 1;
+    const size_t budget = 40960 / sizeof(double);
+    int ab = 0;
+    if constexpr (ab_supported<NX, NU>()) {
+      if (!cached && a.mode != MODE_FWD && kkt_ab_enabled()) {
+        const size_t slot = (size_t)ab_granules<NX, NU>() * 128;
+        const size_t fit = budget > base ? (budget - base) / (waves * slot) : 0;
+        ab = (int)(fit < (size_t)cmax ? fit : (size_t)cmax);
+      }
+    }
+    if (ab > 0) {
+      a.ab_slots = ab;
+      a.lds_base = (int)base;
+      wpb = 1;
+      lds = (base + waves * ab * (size_t)ab_granules<NX, NU>() * 128) * sizeof(double);
+    }
+  }
+  const int block = L > 64 ? L : 64 * wpb;
+  const unsigned grid = (unsigned)((threads + block - 1) / block);
+  if (!a.lds_out && (!a.K || !a.d)) return hipErrorInvalidValue;  // K/d needed as workspace
   if (cached) {
     if (a.tiled)
       hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, CC>), dim3(grid), dim3(block), lds, stream, a);

@@ -30,6 +30,8 @@ struct KKTArgs {
   int ablate;  // timing-only ablation bits (tools/kkt_ablate.py); 0 in every product call
   int tiled;   // 1: A, B, Q, R, M, r, q, c, K, d in the tiled layout (Q, R packed symmetric)
   int lds_out; // set by the launcher: dx/du staged through LDS and written as contiguous rows
+  int ab_slots; // set by the launcher: chunk slots whose A, B stay in LDS (kkt_scan_impl.h: AB)
+  int lds_base; // set by the launcher: LDS offset (doubles) of the A, B / partner slot regions
 };
 
 // On-chip staging of the KKT scan (kkt_scan_impl.h): per trajectory N slots of nu*(nx+1) doubles
@@ -72,6 +74,16 @@ inline int kkt_waves_per_block(long waves, size_t lds_per_wave) {
 inline bool kkt_big_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("NOC_KKT_BIG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// The A, B slots of the SIMD-owning scan instances (kkt_scan_impl.h: AB); NOC_KKT_AB=0 turns
+// them off (read once)
+inline bool kkt_ab_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NOC_KKT_AB");
     return !(e && e[0] == '0');
   }();
   return on;

@@ -280,18 +280,45 @@ def test_ddp_nx8_building_block_loop_matches_oracle():
 @pytest.mark.gpu
 def test_ddp_one_stage_below_the_schedule_floor():
     """ddp(ocp, u, x0, bp) runs at any barrier value (D:98-186 has no bp test); the one-launch
-    kernel used to skip a bp <= 1e-4 as its schedule loop would."""
+    kernel used to skip a bp <= 1e-4 as its schedule loop would.
+
+    Cold start at bp = 5e-5 (pendulum N = 20, seed 5): the GPU needs 145 DDP iterations, the
+    oracle 151.  Root cause (profiles/r05/ddp_flip/): this input is rounding-sensitive.  Perturbing
+    every derivative array and every total cost of the ORACLE by one ulp at random on every
+    evaluation -- the size of the difference between two correct fp64 implementations -- spreads
+    its own count over 145-156 and its final controls by up to 3.1e-3, while the final cost moves
+    by at most 1.7e-10 relative (a flat valley: |Hu| < 1e-4 stops at different points of it)
+    (tools/ddp_jitter_envelope.py, envelope_pendulum20_seed5_bp5e-5.json).  The GPU's trace
+    (tools/ddp_flip_probe.py) agrees with the oracle's on every accept / reject decision for the
+    first 196 passes; by then their predicted reductions differ by up to 5 % (the rounding
+    differences have grown through ~74 non-convex iterations at a tiny barrier), and the first
+    differing decision is a trial at the box constraint's edge (infeasible in one run, feasible in
+    the other).  So the GPU result must lie inside that envelope: count within it (+-1), controls
+    within 1.5x its |dU|, cost within 10x its relative cost spread."""
+    import json
+    import os
     from noc import differential_dynamic_programming as D
     from noc import problems
     from oracle import noc_oracle as O
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = json.load(open(os.path.join(root, "profiles", "r05", "ddp_flip",
+                                      "envelope_pendulum20_seed5_bp5e-5.json")))
     N = 20
     ocp = problems.pendulum(1.0 / N)
     x0, u0 = problems.initial_conditions("pendulum", N, 1, seed=5)
-    # warm start from the schedule's solution: a cold start at bp = 5e-5 runs ~150 non-convex
-    # iterations whose count rounding decides (see test_ddp_matches_oracle)
+    X, U, its = D.ddp(ocp, u0[0], x0[0], 5e-5)
+    prob = _oracle_problem("pendulum", N)
+    Xr, Ur, itr, _ = O.ddp(prob, u0[0], x0[0], 5e-5)
+    assert itr == env["oracle_iterations"]
+    lo, hi = min(env["jittered_iterations"]), max(env["jittered_iterations"])
+    assert lo - 1 <= its <= hi + 1, (its, lo, hi)
+    assert np.max(np.abs(U - Ur)) <= 1.5 * env["max_abs_dU"]
+    c = prob.total_cost(O.rollout(prob.dynamics, U, x0[0]), U, 5e-5)
+    assert abs(c - env["oracle_cost"]) <= 10 * env["max_rel_dcost"] * abs(env["oracle_cost"])
+    # warm start from the schedule's solution: a well-conditioned input, oracle count within one
     Uw, _ = D.interior_point_ddp(ocp, u0[0], x0[0])
     X, U, its = D.ddp(ocp, Uw, x0[0], 5e-5)
-    Xr, Ur, itr, _ = O.ddp(_oracle_problem("pendulum", N), Uw, x0[0], 5e-5)
+    Xr, Ur, itr, _ = O.ddp(prob, Uw, x0[0], 5e-5)
     assert its >= 1 and abs(its - itr) <= 1, (its, itr)
     assert np.max(np.abs(U - Ur)) < 1e-5
 

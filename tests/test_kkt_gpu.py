@@ -426,3 +426,58 @@ def test_kkt_random_shapes_match_oracle():
         assert np.array_equal(out["feasible"].astype(bool), ref["feasible"].astype(bool))
 
     check()
+
+
+@pytest.mark.parametrize("N,lanes,B,affine", [(200, 64, 1024, False), (200, 32, 2048, False),
+                                              (7, 64, 33, True), (250, 64, 1000, True),
+                                              (1, 32, 5, False), (65, 32, 9, True)])
+@pytest.mark.parametrize("tiled", [True, False])
+def test_ab_slots_equal_rereads(N, lanes, B, affine, tiled):
+    """The 512-register instances (L = 32 / 64 with waves <= SIMDs) park A, B of the first chunk
+    slots in LDS in phase 1 and read them back in phases 3 and 4 instead of re-reading them.
+    Ablation bit 6 turns the slots off.  Tiled layout (the product path: the interior-point
+    workspace and the bench): every output bit-identical.  Natural layout: the two code paths
+    contract a few FMAs differently (results differ in the last bits, 1.6e-15 measured,
+    tools/probes/ab_debug.py), so within 16 eps; both match the oracle on a sample.  Covers
+    ragged chunks (N % L), affine terms and N < L."""
+    from noc import lqt, _lib
+    case = rand_lq(4200 + N + lanes + B, B, N, 4, 1, affine=affine)
+    g = lambda k: dev(case.get(k))
+    lib = _lib.load()
+
+    def solve():
+        if tiled and not affine:
+            tb = lqt.to_tiled(g("A"), g("B"), g("Q"), g("R"), g("M"), g("r"), g("P"), lanes)
+            return lqt.kkt_solve_tiled(tb, reg=g("reg"), want_value=True)
+        return lqt.kkt_solve(g("A"), g("B"), g("Q"), g("R"), g("M"), g("r"), g("P"), reg=g("reg"),
+                             x0=g("x0"), q=g("q"), c=g("c"), p=g("p"), lanes=lanes, want_value=True)
+    try:
+        parked = solve()
+        lib.noc_debug_set_ablation(64)
+        reread = solve()
+    finally:
+        lib.noc_debug_set_ablation(0)
+    torch.cuda.synchronize()
+    exact = tiled and not affine
+    eps = float(np.finfo(np.float64).eps)
+
+    def same(x, y, k):
+        if exact:
+            assert torch.equal(x, y), k
+        else:
+            scale = max(1.0, float(y.abs().max()))
+            assert float((x - y).abs().max()) <= 16 * eps * scale, k
+
+    for k in ("dx", "du", "pred", "S", "v"):
+        same(getattr(parked, k), getattr(reread, k), k)
+    assert torch.equal(parked.feasible, reread.feasible)
+    if exact:  # the tiled K, d buffers have padding slots nobody writes
+        gains = lambda r: (lqt.untile(r.K, (B, N, 1, 4), lanes), lqt.untile(r.d, (B, N, 1), lanes))
+    else:
+        gains = lambda r: (r.K, r.d)
+    for x, y in zip(gains(parked), gains(reread)):
+        same(x, y, "K/d")
+    sample = sorted({0, B // 2, B - 1})
+    ref = oracle_batch({k: v[sample] for k, v in case.items()})
+    for k in ("dx", "du", "pred"):
+        assert relerr(getattr(parked, k)[sample].cpu(), ref[k]) < RTOL, k
