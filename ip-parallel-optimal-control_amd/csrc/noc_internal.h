@@ -23,6 +23,7 @@ enum KKTMode : int { MODE_FULL = 0, MODE_BWD = 1, MODE_FWD = 2 };
 // Kernel argument block of the KKT scan (passed by value).  Layouts: include/noc_hip.h.
 struct KKTArgs {
   int N, B, mode;
+  int ab_slots; // set by the launcher: chunk slots whose A, B stay in LDS (kkt_scan_impl.h: AB)
   const double *A, *Bm, *Q, *R, *M, *r, *q, *c, *P, *p, *x0, *reg;
   const int* active;
   double *dx, *du, *pred, *K, *d, *S, *v;
@@ -30,8 +31,9 @@ struct KKTArgs {
   int ablate;  // timing-only ablation bits (tools/kkt_ablate.py); 0 in every product call
   int tiled;   // 1: A, B, Q, R, M, r, q, c, K, d in the tiled layout (Q, R packed symmetric)
   int lds_out; // set by the launcher: dx/du staged through LDS and written as contiguous rows
-  int ab_slots; // set by the launcher: chunk slots whose A, B stay in LDS (kkt_scan_impl.h: AB)
-  int lds_base; // set by the launcher: LDS offset (doubles) of the A, B / partner slot regions
+  int lds_base; // set by the launcher: LDS offset (doubles) of the A, B slot region
+  // (ab_slots and lds_base sit in what was alignment padding: the struct -- the scan kernels'
+  // argument block -- keeps its round-4 size)
 };
 
 // On-chip staging of the KKT scan (kkt_scan_impl.h): per trajectory N slots of nu*(nx+1) doubles
