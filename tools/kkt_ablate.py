@@ -17,7 +17,9 @@ lib = _lib.load()
 out = lqt.kkt_solve_tiled(tb, reg=blk["reg"], want_gains=(lanes == 1))
 variants = {"full": 0, "streamed": 8, "no_fwd": 2, "no_scan": 1, "no_scan_no_fwd": 3,
             "phase1_only": 5, "phase1+2": 4, "hot_rereads": 16}
-if lanes == 1:  # the group solve (kkt_group8_impl.h): backward sweep / forward sweep split
+if os.environ.get("ABLATE_VARIANTS"):  # e.g. '{"full": 0, "prio_mem": 128}'
+    variants = json.loads(os.environ["ABLATE_VARIANTS"])
+elif lanes == 1:  # the group solve (kkt_group8_impl.h): backward sweep / forward sweep split
     variants = {"full": 0, "no_fwd": 2, "fwd_only": 64}
 REPS = 10
 graphs = {}
