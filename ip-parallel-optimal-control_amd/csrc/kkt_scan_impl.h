@@ -83,10 +83,20 @@ struct Elem {
   Sym<NX> J;
 };
 
+// tiled load with the cache policy of a last use (LAST: non-temporal) or the default one
+template <int E, int L, bool LAST>
+NOC_DEV void tload_pol(const double* __restrict__ base, int traj, int j, int l, int cmax, double* dst) {
+  if constexpr (LAST) tload_last<E, L>(base, traj, j, l, cmax, dst);
+  else tload<E, L>(base, traj, j, l, cmax, dst);
+}
+
 // PART: 0 = the whole stage, 1 = everything but Q, 2 = Q only (phase 3 prefetches part 1 of the
 // next stage and loads Q, which the Riccati step uses last, at the top of the current one),
-// 3 = everything but A, B (the scan instances that keep A, B on chip: kkt_scan_wave_src, AB)
-template <int NX, int NU, int L, bool AFF, bool TILED, int PART = 0>
+// 3 = everything but A, B (the scan instances that keep A, B on chip: kkt_scan_wave_src, AB).
+// LAST (phase 3, tiled): the solve's last read of Q, R, M, r, q -- non-temporal, so the lines
+// they bring in do not displace blocks still to be re-read (other waves' chunks, this wave's A,
+// B, c for phase 4) from the memory-side cache; A, B, c keep the default policy
+template <int NX, int NU, int L, bool AFF, bool TILED, int PART = 0, bool LAST = false>
 NOC_DEV void load_stage(const KKTArgs& a, int traj, size_t si, int j, int l, int cmax, double reg,
                         StageData<NX, NU>& st) {
   constexpr bool REST = PART != 2, WQ = PART != 1, WAB = REST && PART != 3;
@@ -95,13 +105,13 @@ NOC_DEV void load_stage(const KKTArgs& a, int traj, size_t si, int j, int l, int
       tload<NX * NX, L>(a.A, traj, j, l, cmax, st.A.v);
       tload<NX * NU, L>(a.Bm, traj, j, l, cmax, st.B.v);
     }
-    if constexpr (WQ) tload<Sym<NX>::SZ, L>(a.Q, traj, j, l, cmax, st.Q.v);
+    if constexpr (WQ) tload_pol<Sym<NX>::SZ, L, LAST>(a.Q, traj, j, l, cmax, st.Q.v);
     if constexpr (REST) {
-      tload<Sym<NU>::SZ, L>(a.R, traj, j, l, cmax, st.R.v);
-      tload<NX * NU, L>(a.M, traj, j, l, cmax, st.M.v);
-      tload<NU, L>(a.r, traj, j, l, cmax, st.r.v);
+      tload_pol<Sym<NU>::SZ, L, LAST>(a.R, traj, j, l, cmax, st.R.v);
+      tload_pol<NX * NU, L, LAST>(a.M, traj, j, l, cmax, st.M.v);
+      tload_pol<NU, L, LAST>(a.r, traj, j, l, cmax, st.r.v);
       if constexpr (AFF) {
-        if (a.q) tload<NX, L>(a.q, traj, j, l, cmax, st.q.v); else set_zero(st.q);
+        if (a.q) tload_pol<NX, L, LAST>(a.q, traj, j, l, cmax, st.q.v); else set_zero(st.q);
         if (a.c) tload<NX, L>(a.c, traj, j, l, cmax, st.c.v); else set_zero(st.c);
       }
     }
@@ -550,9 +560,12 @@ struct ArgsSrc {
   NOC_DEV void stage(int s, int j, double reg, StageData<NX, NU>& st) const {
     load_stage<NX, NU, L, AFF, TILED>(a, traj, tN + s, j, l, cmax, reg, st);
   }
-  template <int PART>
+  template <int PART, bool LAST = false>
   NOC_DEV void stage_part(int s, int j, double reg, StageData<NX, NU>& st) const {
-    load_stage<NX, NU, L, AFF, TILED, PART>(a, traj, tN + s, j, l, cmax, reg, st);
+    load_stage<NX, NU, L, AFF, TILED, PART, LAST>(a, traj, tN + s, j, l, cmax, reg, st);
+  }
+  NOC_DEV void stage_last(int s, int j, double reg, StageData<NX, NU>& st) const {  // phase 3
+    load_stage<NX, NU, L, AFF, TILED, 0, true>(a, traj, tN + s, j, l, cmax, reg, st);
   }
   NOC_DEV void ab(int s, int j, Mat<NX, NX>& A, Mat<NX, NU>& Bm, Vec<NX>& c) const {
     load_AB<NX, NU, L, AFF, TILED>(a, traj, tN + s, j, l, cmax, A, Bm, c);
@@ -579,7 +592,7 @@ struct ArgsSrc {
 // (lds_ab); a.ab_slots = 0 turns it off at run time.  Not in the two-wave segments (L = 128): their
 // re-reads are L2 hits already, and the slots measured +2.5 % there (profiles/r05/ab_slots/).
 template <int NX, int NU, int L, bool AFF, bool TILED, class SRC, int CACHE = 0, bool HANDOFF = true,
-          bool BIG = false, bool AB = (BIG && ab_supported<NX, NU>())>
+          bool BIG = false, bool NT3 = false, bool AB = (BIG && ab_supported<NX, NU>())>
 NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, const SRC& src) {
   constexpr int KD = kd_width<NX, NU>();
   if (traj >= a.B) return;                     // uniform over the segment
@@ -718,7 +731,12 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     double pred = 0.0;
     int feas = 1;
     double* skd = lds_slots<NX, NU, L>(N);  // K, d stay on chip for phase 4 when staged
-    auto stage3 = [&](int s, StageData<NX, NU>& st) { src_re.stage(s, s - start, reg, st); };
+    // phase 3's re-read of a stage: the last use of Q, R, M, r, q -- non-temporal in the NT3
+    // instances (the launcher's cache policy, kkt_nt3)
+    auto stage3 = [&](int s, StageData<NX, NU>& st) {
+      if constexpr (NT3) src_re.stage_last(s, s - start, reg, st);
+      else src_re.stage(s, s - start, reg, st);
+    };
     auto riccati_stage = [&](const int s, const StageData<NX, NU>& st) {
       Mat<NX, NX> SA;
       Mat<NX, NU> SB;
@@ -841,12 +859,12 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
           const int jl = len < abn ? len : abn;
           for (int s = start + len - 1; s >= start + jl; --s) {
             StageData<NX, NU> st;
-            src_re.stage(s, s - start, reg, st);
+            stage3(s, st);
             riccati_stage(s, st);
           }
           for (int s = start + jl - 1; s >= start; --s) {
             StageData<NX, NU> st;
-            src_re.template stage_part<3>(s, s - start, reg, st);
+            src_re.template stage_part<3, NT3>(s, s - start, reg, st);
             ab_load<NX, NU>(lab, s - start, st.A, st.B);
             riccati_stage(s, st);
           }
@@ -1124,18 +1142,18 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
 }
 
 template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE = 0, bool HANDOFF = true,
-          bool BIG = false>
+          bool BIG = false, bool NT3 = false>
 NOC_DEV void kkt_scan_wave(const KKTArgs& a, const int traj, const int l) {
   const int cmax = a.N / L + (a.N % L ? 1 : 0);
   const ArgsSrc<NX, NU, L, AFF, TILED> src{a, traj, l, cmax, (size_t)traj * a.N};
-  kkt_scan_wave_src<NX, NU, L, AFF, TILED, ArgsSrc<NX, NU, L, AFF, TILED>, CACHE, HANDOFF, BIG>(a, traj, l,
-                                                                                          src);
+  kkt_scan_wave_src<NX, NU, L, AFF, TILED, ArgsSrc<NX, NU, L, AFF, TILED>, CACHE, HANDOFF, BIG, NT3>(a, traj,
+                                                                                               l, src);
 }
 
 // BIG (L = 32, 64; nx = 3, 4): one wave per SIMD -- for batches whose waves all fit one per SIMD
 // anyway (the 2048- and 1024-per-GPU shards): 512 registers (no spill) and masked combines, like
 // the two-wave segments.
-template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE, bool BIG = false>
+template <int NX, int NU, int L, bool AFF, bool TILED, int CACHE, bool BIG = false, bool NT3 = false>
 __global__ __launch_bounds__(L > 64 ? L : 256, (L > 64 || BIG) ? 1 : NOC_KKT_WAVES_PER_SIMD) void kkt_scan_kernel(KKTArgs a) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   // Two-wave segments (L = 128) must put their two waves on DIFFERENT SIMDs: with <= 256
@@ -1162,7 +1180,7 @@ __global__ __launch_bounds__(L > 64 ? L : 256, (L > 64 || BIG) ? 1 : NOC_KKT_WAV
       return;
     }
   }
-  kkt_scan_wave<NX, NU, L, AFF, TILED, CACHE, true, BIG>(a, traj, tid % L);
+  kkt_scan_wave<NX, NU, L, AFF, TILED, CACHE, true, BIG, NT3 && TILED && CACHE == 0>(a, traj, tid % L);
 }
 
 // Register-cached chunk length for (NX, NU, L): only where a short chunk's blocks fit beside the
@@ -1231,11 +1249,18 @@ hipError_t launch_kkt(const KKTArgs& a_in, hipStream_t stream) {
       else
         hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, false, 0, true>), dim3(grid), dim3(block), lds, stream, a);
     }
-  } else {
-    if (a.tiled)
-      hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, 0>), dim3(grid), dim3(block), lds, stream, a);
+  } else if (!a.tiled) {
+    hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, false, 0>), dim3(grid), dim3(block), lds, stream, a);
+  } else if constexpr (L > 64) {  // two-wave segments: non-temporal (kkt_nt3)
+    hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, 0, false, true>), dim3(grid), dim3(block), lds, stream, a);
+  } else if constexpr (L == 32) {  // both policies, by the batch's size (kkt_nt3)
+    if (kkt_nt3(a.B, a.N, NX, NU))
+      hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, 0, false, true>), dim3(grid), dim3(block), lds, stream,
+                         a);
     else
-      hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, false, 0>), dim3(grid), dim3(block), lds, stream, a);
+      hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, 0>), dim3(grid), dim3(block), lds, stream, a);
+  } else {
+    hipLaunchKernelGGL((kkt_scan_kernel<NX, NU, L, AFF, true, 0>), dim3(grid), dim3(block), lds, stream, a);
   }
   return hipGetLastError();
 }

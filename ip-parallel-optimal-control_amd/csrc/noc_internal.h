@@ -91,6 +91,29 @@ inline bool kkt_ab_enabled() {
   return on;
 }
 
+// Cache policy of the scan's phase-3 re-reads (the last use of Q, R, M, r, q; tiled layout):
+// non-temporal or the default.  Measured, same build, bench lines (profiles/r05/nt3/):
+// non-temporal pays where a launch's blocks overflow the 256 MiB memory-side cache by far -- their
+// lines would only displace the A, B, c that phase 4 and the other waves' phase 3 still re-read
+// (c5, 577 MB: -4.2 %; N = 300, 432 MB: -0.9 %; 16 384 cart-poles: -1.3 %) -- and in the
+// two-wave segments of the 512 shard, whose re-reads are cache hits (-2.0 %); it costs where a
+// good part of the batch survives in that cache from one launch to the next (c3, 288 MB: +0.8 %;
+// 4096 cart-poles at N = 100, 144 MB: +2.8 %).  The 512-register instances stay at the default
+// (1024 shard 0; 2048 shard -1.0 % as a run-time choice inside one kernel, +1.5 % as an instance
+// of its own).  So the two-wave (L = 128) instance is built non-temporal, and the L = 32 instance
+// of larger batches exists in both forms, chosen here by the blocks' size: non-temporal beyond
+// 1.5x the cache.  NOC_KKT_NT3=0 | 1 forces that choice (read once).
+inline bool kkt_nt3(int B, int N, int nx, int nu) {
+  static const int forced = [] {
+    const char* e = std::getenv("NOC_KKT_NT3");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  if (forced >= 0) return forced == 1;
+  const double stage = 8.0 * (nx * nx + 2 * nx * nu + nx * (nx + 1) / 2 + nu * (nu + 1) / 2 + nu + 2 * nx);
+  const double mall = 256.0 * 1024 * 1024;  // MI355X Infinity Cache
+  return (double)B * N * stage > 1.5 * mall;
+}
+
 inline size_t kkt_lds_bytes_rt(int nx, int nu, int N, int L) {
   if (L < 8) return 0;  // lanes = 1 (group solve): gains go through HBM
   const size_t per_traj = (size_t)(((long long)N * nu * (nx + 1) + nx + 1) & ~1LL);

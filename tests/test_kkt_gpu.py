@@ -337,6 +337,31 @@ def test_full_size_bench_blocks_properties(name, N, B, lanes):
     assert relerr(res.pred[sample].cpu(), ref["pred"]) < RTOL
 
 
+def test_nontemporal_phase3_instance_is_bit_identical():
+    """The L = 32 scan of a batch whose blocks exceed 1.5x the memory-side cache runs the instance
+    that reads phase 3's Q, R, M, r non-temporally (kkt_nt3 in csrc/noc_internal.h) -- a cache
+    policy, not an arithmetic change.  The first 4096 trajectories of an 8192-trajectory batch (577
+    MB of blocks: that instance) equal the same 4096 solved as a batch of their own (288 MB: the
+    default instance) bit for bit, and the 8192 match the oracle on a sample."""
+    from noc import lqt
+    from noc.problems import make_bench_blocks
+    B, H = 8192, 4096
+    blocks = make_bench_blocks("cartpole", N=200, batch=B, seed=9, lanes=32)
+    nat = blocks["engine"].natural_blocks()
+    full = lqt.kkt_solve_tiled(blocks["tiled"], reg=blocks["reg"], want_gains=False)
+    half_tb = lqt.to_tiled(*(nat[k][:H] for k in ("A", "B", "Q", "R", "M", "r", "P")), lanes=32)
+    half = lqt.kkt_solve_tiled(half_tb, reg=blocks["reg"][:H], want_gains=False)
+    torch.cuda.synchronize()
+    for k in ("dx", "du", "pred", "feasible"):
+        assert torch.equal(getattr(full, k)[:H], getattr(half, k)), k
+    sample = [0, 3000, 4095, 4096, 6001, B - 1]
+    case = {k: nat[k][sample].cpu().numpy() for k in ["A", "B", "Q", "R", "M", "r", "P"]}
+    case["reg"] = blocks["reg"][sample].cpu().numpy()
+    ref = oracle_batch(case)
+    assert relerr(full.dx[sample].cpu(), ref["dx"]) < RTOL
+    assert relerr(full.du[sample].cpu(), ref["du"]) < RTOL
+
+
 def _lm_lqt(T):
     """examples/linear_mpc_parallel.py:24-64: RK4 double integrator (step 0.001), Q = P =
     diag(1e2, 1), R = 0.1, tracking zero."""
