@@ -64,9 +64,14 @@ NOC_DEV unsigned dma_off(int sz, int rb, int rows, int i, int lane, int traj0, i
   return (unsigned)((size_t)t * N * sz + row * rb + off);
 }
 
+// AUX: the DMA's cache policy bits -- kLastUse (nt) for the backward sweep's last read of a field
+template <int AUX = 0>
 NOC_DEV void glds16(const char* src, char* lds_dst) {
-  __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)lds_dst, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)lds_dst, 16, 0, AUX);
 }
+// Q, R, M, r, q are read for the last time by the backward sweep (the forward sweep re-reads A, B,
+// c): non-temporal, so their lines do not displace A, B, c from the caches before that re-read
+constexpr int kLastUse = 2;
 
 // stages of the forward sweep's loads in flight per wave (deeper rings spill)
 constexpr int kFwdDepth = 2;
@@ -149,19 +154,19 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
       const char* bB = ubase(a.Bm, 256, s);
       NOC_UNROLL for (int i = 0; i < 4; ++i) glds16(bA + oA[i], base + OA + i * 1024);
       if constexpr (TILED) {
-        glds16(bQ + oQ[0], base + OQ);
-        glds16(bQ + oQ[1], base + OQ + 1024);
-        if (lane < 16) glds16(bQ + oQ[2], base + OQ + 2048);
+        glds16<kLastUse>(bQ + oQ[0], base + OQ);
+        glds16<kLastUse>(bQ + oQ[1], base + OQ + 1024);
+        if (lane < 16) glds16<kLastUse>(bQ + oQ[2], base + OQ + 2048);
       } else {
-        NOC_UNROLL for (int i = 0; i < 4; ++i) glds16(bQ + oQ[i], base + OQ + i * 1024);
+        NOC_UNROLL for (int i = 0; i < 4; ++i) glds16<kLastUse>(bQ + oQ[i], base + OQ + i * 1024);
       }
       NOC_UNROLL for (int i = 0; i < 2; ++i) glds16(bB + oB[i], base + OB + i * 1024);
-      if (!TILED || lane < 40) glds16(ubase(a.R, LD::RB, s) + oR, base + OR);
-      if (lane < 16) glds16(ubase(a.r, 32, s) + orv, base + ORV);
+      if (!TILED || lane < 40) glds16<kLastUse>(ubase(a.R, LD::RB, s) + oR, base + OR);
+      if (lane < 16) glds16<kLastUse>(ubase(a.r, 32, s) + orv, base + ORV);
       if constexpr (AFF) {
         if (lane < 32) {
           glds16(ubase(a.c ? a.c : a.A, 64, s) + ocq, base + OC);
-          glds16(ubase(a.q ? a.q : a.A, 64, s) + ocq, base + OQV);
+          glds16<kLastUse>(ubase(a.q ? a.q : a.A, 64, s) + ocq, base + OQV);
         }
       }
     };
@@ -182,7 +187,12 @@ __global__ __launch_bounds__(64, NOC_GROUP8_WAVES_PER_SIMD) void kkt_group8_kern
     // row q of M (stage s) straight into registers, one stage ahead like the DMA
     auto load_mrow = [&](int s, double* m) {
       const size_t mb = TILED ? group_base(NX * NU, N, trajc, s) : ((size_t)trajc * N + s) * (NX * NU);
-      gload<NU>(a.M + mb + q * NU, m);
+      const noc_dbl2* mp = reinterpret_cast<const noc_dbl2*>(a.M + mb + q * NU);  // last use: nt
+      NOC_UNROLL for (int i = 0; i < NU / 2; ++i) {
+        const noc_dbl2 t = __builtin_nontemporal_load(mp + i);
+        m[2 * i] = t.x;
+        m[2 * i + 1] = t.y;
+      }
     };
     // The M row is prefetched a stage ahead like the DMA and lands with it.  (Loaded at the top
     // of its own stage, its first use waited vmcnt(0): the compiler does not count the LDS-DMA
