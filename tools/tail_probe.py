@@ -42,7 +42,7 @@ if "prof" in os.environ.get("NOC_HIP_LIB", ""):  # per-trajectory start / end (1
     tt = np.frombuffer(buf, dtype=np.int64).reshape(n, 2).astype(np.float64)
     t0 = tt[:, 0].min()
     start_ms, end_ms = (tt[:, 0] - t0) * 1e-5, (tt[:, 1] - t0) * 1e-5
-    np.save(os.path.join(a.out, f"{a.problem}_N{a.N}_B{a.B}_times_ms.npy"),
+    np.save(os.path.join(a.out, f"{a.problem}_N{a.N}_B{a.B}{os.environ.get('NOC_PERSIST_HEAVY', '')}_times_ms.npy"),
             np.stack([start_ms, end_ms], 1))
     k = int(solves.argmax())
     z = int(end_ms.argmax())
@@ -56,11 +56,15 @@ if "prof" in os.environ.get("NOC_HIP_LIB", ""):  # per-trajectory start / end (1
                                       if r < a.B},
                 "us_per_solve_p50": float(np.median(1e3 * (end_ms - start_ms) / solves))}
 its = eng.t["total_it"].cpu().numpy()
-np.save(os.path.join(a.out, f"{a.problem}_N{a.N}_B{a.B}_solves.npy"), solves)
+tag = os.environ.get("NOC_PERSIST_HEAVY", "")
+tag = f"_h{tag}" if tag else ""
+np.save(os.path.join(a.out, f"{a.problem}_N{a.N}_B{a.B}{tag}_solves.npy"), solves)
+if getattr(eng, "_order", None) is not None:  # the launch order (descending initial cost)
+    np.save(os.path.join(a.out, f"{a.problem}_N{a.N}_B{a.B}{tag}_order.npy"), eng._order.cpu().numpy())
 q = np.percentile(solves, [50, 90, 99, 99.9, 100])
 print(json.dumps({"problem": a.problem, "N": a.N, "B": a.B, "wall_ms": ms,
                   "kkt_solves_computed": int(solves.sum()), "mean": float(solves.mean()),
                   "p50_p90_p99_p999_max": [float(v) for v in q],
                   "n_over_300": int((solves > 300).sum()), "n_over_400": int((solves > 400).sum()),
                   "argmax": int(solves.argmax()), "mean_iters": float(its.mean()),
-                  "env_wide": os.environ.get("NOC_PERSIST_WIDE"), "timeline": timeline}), flush=True)
+                  "env_wide": os.environ.get("NOC_PERSIST_WIDE"), "env_heavy": os.environ.get("NOC_PERSIST_HEAVY"), "timeline": timeline}), flush=True)
