@@ -169,6 +169,9 @@ class BatchedIPM:
         self.prepare(mode, terminal)
         return torch.argsort(self.t["cost"], descending=True, stable=True).to(torch.int32)
 
+    # KKT solves of the probe launch of schedule="probe" (see solve_persistent)
+    PROBE_SOLVES = 10
+
     def solve_persistent(self, mode: int = _lib.MODE_PAR, terminal: Optional[int] = None,
                          bp0: float = 0.1, max_solves: int = 10 ** 7, resume: bool = False,
                          schedule: str = "auto"):
@@ -178,19 +181,39 @@ class BatchedIPM:
         resume=True continues every trajectory from the workspace state a previous (capped)
         solve left (NOC_WS_RESUME); max_solves counts the solves of both.
         schedule: "index" launches trajectory i as workgroup i; "cost" launches them by
-        descending initial cost (launch_order, ws.order); "auto" = "cost" when the batch exceeds
-        the resident waves and this is not a resume.  Every trajectory's result is the same
-        either way (independent, deterministic); only the schedule changes."""
+        descending initial cost (launch_order, ws.order); "probe" runs every trajectory's first
+        PROBE_SOLVES KKT solves in one capped launch and resumes the rest ordered by descending
+        total cost at that point, which predicts the remaining solves far better than the initial
+        cost does (c3: correlation 0.86 vs 0.3; profiles/r05/probe_order/); "auto" = "probe" when
+        the batch exceeds the resident waves and this is not a resume.  Every trajectory's result
+        is the same either way (independent, deterministic, and a capped-and-resumed solve equals
+        an uninterrupted one bit for bit); only the schedule changes."""
         terminal = default_terminal(mode) if terminal is None else terminal
-        if schedule not in ("auto", "cost", "index"):
+        if schedule not in ("auto", "cost", "index", "probe"):
             raise ValueError(schedule)
-        ordered = not resume and (schedule == "cost" or (
-            schedule == "auto" and self.Bt > self._resident_slots()))
+        if schedule == "auto":
+            schedule = "probe" if (not resume and self.Bt > self._resident_slots()) else "index"
+        if schedule == "probe" and not resume:
+            k = min(int(self.PROBE_SOLVES), int(max_solves))
+            self._launch(mode, terminal, bp0, k, resume=False, order=None)
+            if k >= max_solves:
+                self._order = None
+                return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
+            # trajectories already done leave at once; the rest start costliest first
+            self._order = torch.argsort(self.t["cost"], descending=True, stable=True).to(torch.int32)
+            self._launch(mode, terminal, bp0, max_solves, resume=True, order=self._order)
+            return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
+        ordered = not resume and schedule == "cost"
         self._order = self.launch_order(mode, terminal, bp0) if ordered else None
+        self._launch(mode, terminal, bp0, max_solves, resume=resume, order=self._order)
+        return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
+
+    def _launch(self, mode, terminal, bp0, max_solves, resume, order):
+        """one noc_ipm_solve (resume: NOC_WS_RESUME; order: ws.order, a permutation or None)"""
         flags = self.ws.flags
         if resume:
             self.ws.flags = flags | _lib.WS_RESUME
-        self.ws.order = self._order.data_ptr() if ordered else None
+        self.ws.order = order.data_ptr() if order is not None else None
         try:
             _lib.check(self._lib.noc_ipm_solve(ctypes.byref(self.fam_c), ctypes.byref(self.ws),
                                                mode, terminal, float(bp0), int(max_solves),
@@ -198,7 +221,6 @@ class BatchedIPM:
         finally:
             self.ws.flags = flags
             self.ws.order = None
-        return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
 
     def solve(self, mode: int = _lib.MODE_PAR, terminal: Optional[int] = None,
               bp0: float = 0.1, poll_every: int = 8, max_steps: Optional[int] = None):

@@ -454,6 +454,32 @@ def test_cost_ordered_launch_gives_identical_results():
         assert np.array_equal(res["index"][k], res["cost"][k]), k
 
 
+@pytest.mark.parametrize("probe", [1, 7, 10])
+def test_probe_ordered_launch_gives_identical_results(probe):
+    """schedule="probe" (the default beyond the resident waves): a capped launch of every
+    trajectory's first PROBE_SOLVES KKT solves, then the rest resumed by descending total cost --
+    bit-identical to the single index-order launch (a capped-and-resumed solve equals the
+    uninterrupted one); the resumed launch really is reordered."""
+    from noc.ipm import BatchedIPM
+    N, Bt = 60, 96
+    ocp, x0, u0 = _resume_case("cartpole", N, Bt, seed=8)
+    keys = ("u", "x", "kkt_solves", "total_it", "phase", "bp", "rp", "rinc", "repeats", "it")
+    res = {}
+    for sched in ("index", "probe"):
+        eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
+        eng.PROBE_SOLVES = probe
+        eng.load(u0, x0)
+        eng.solve_persistent(schedule=sched)
+        torch.cuda.synchronize()
+        res[sched] = {k: eng.t[k].cpu().numpy().copy() for k in keys}
+        if sched == "probe":
+            order = eng._order.cpu().numpy()
+            assert sorted(order.tolist()) == list(range(Bt)) and order.tolist() != list(range(Bt))
+    assert (res["index"]["phase"] == 3).all()
+    for k in keys:
+        assert np.array_equal(res["index"][k], res["probe"][k]), k
+
+
 def test_linear8_ipm_uses_group_solve_and_is_exact():
     """Four stacked double integrators (nx=8, nu=4; the c4 family): the IPM workspace defaults to
     the grouped layout + horizon-sequential group solve (lanes 1); the unconstrained LQ problem is
