@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 5 final, part c (after the probe-ordered persistent launch; kernels unchanged since
+# final3): every GPU test, smoke, the default bench line.
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+cd "$R"; O=gpurun_out/${OUT:-r5final_c}; mkdir -p $O
+export TMPDIR=/tmp
+run() { local t=$1; local log=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$log" 2>&1; local rc=$?; echo "rc=$rc $log"; tail -1 "$O/$log" | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi; }
+run 900 pytest_gpu.txt python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf
+run 200 smoke.txt python -c "import __graft_entry__ as g; g.smoke()"
+run 300 bench_c3.txt python bench.py
+run 300 bench_torchrun1.txt python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --steps 20 --warmup 3 --no-cpu
