@@ -200,54 +200,60 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
           gload<NX>(X + (size_t)k * NX, x);
           NOC_UNROLL for (int i = 0; i < NU; ++i) u[i] = U[(size_t)k * NU + i];
         };
-        if (pair) {  // loads, then both computations, then the stores: one basic block of work
-          for (int j = 0; j < cmax; j += 2) {
+        // The costates are a reverse affine scan (C:34-54) fused with the LQ blocks (P:31-42).
+        // Its in-chunk fold (G, g) <- (A' G, cx + A' g) runs inside the linearisation, which
+        // walks the chunk backwards for it, on the A, cx it has just computed -- the same
+        // operations in the same order as a separate pass reading them back from the workspace,
+        // without that pass's loads (the solve moves ~6.5 TB/s at c3).
+        Mat<NX, NX> G;
+        Vec<NX> g;
+        set_identity(G);
+        set_zero(g);
+        auto fold = [&](const LinOut& o, bool valid) {
+          Mat<NX, NX> Gn;
+          Vec<NX> gn;
+          NOC_UNROLL for (int i = 0; i < NX; ++i) {
+            double t = o.cx[i];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) t += o.fx[m * NX + i] * g[m];
+            gn[i] = t;
+            NOC_UNROLL for (int jj = 0; jj < NX; ++jj) {
+              double u = 0.0;
+              NOC_UNROLL for (int m = 0; m < NX; ++m) u += o.fx[m * NX + i] * G(m, jj);
+              Gn(i, jj) = u;
+            }
+          }
+          NOC_UNROLL for (int i = 0; i < NX * NX; ++i) G.v[i] = valid ? Gn.v[i] : G.v[i];
+          NOC_UNROLL for (int i = 0; i < NX; ++i) g.v[i] = valid ? gn.v[i] : g.v[i];
+        };
+        if (pair) {  // descending pairs over the wave-uniform chunk bound: loads, then both
+                     // computations, then the stores and the fold (one basic block of work)
+          for (int j = cmax - 1; j >= 0; j -= 2) {
             double x0[NX], u0[NU], x1[NX], u1[NU];
             load_xu(clampk(start + j), x0, u0);
-            load_xu(clampk(start + j + 1), x1, u1);
+            load_xu(clampk(start + (j - 1 >= 0 ? j - 1 : j)), x1, u1);
+            const bool v0 = j < len, v1 = j - 1 >= 0 && j - 1 < len;
             LinOut o0, o1;
             lin_compute(x0, u0, o0);
             lin_compute(x1, u1, o1);
-            if (j < len) lin_store(j, o0);
-            if (j + 1 < len) lin_store(j + 1, o1);
+            if (v0) lin_store(j, o0);
+            if (v1) lin_store(j - 1, o1);
+            fold(o0, v0);
+            fold(o1, v1);
           }
         } else {
-          for (int j = 0; j < len; ++j) {
+          for (int j = len - 1; j >= 0; --j) {
             double x[NX], u[NU];
             load_xu(start + j, x, u);
             LinOut o;
             lin_compute(x, u, o);
             lin_store(j, o);
+            fold(o, true);
           }
         }
         NOC_PHASE(1);
-        // costates as a reverse affine scan (C:34-54) fused with the LQ blocks (P:31-42)
         const double* xN = X + (size_t)N * NX;
         double lamN[NX];
         f.final_grad(xN, lamN);  // grad(final_cost) (C:35)
-        Mat<NX, NX> G;
-        Vec<NX> g;
-        set_identity(G);
-        set_zero(g);
-        for (int j = len - 1; j >= 0; --j) {
-          double A[NX * NX], cx[NX];
-          tload<NX * NX, PL>(w.A, b, j, l, cmax, A);
-          tload<NX, PL>(w.cx, b, j, l, cmax, cx);
-          Mat<NX, NX> Gn;
-          Vec<NX> gn;
-          NOC_UNROLL for (int i = 0; i < NX; ++i) {
-            double t = cx[i];
-            NOC_UNROLL for (int m = 0; m < NX; ++m) t += A[m * NX + i] * g[m];
-            gn[i] = t;
-            NOC_UNROLL for (int jj = 0; jj < NX; ++jj) {
-              double u = 0.0;
-              NOC_UNROLL for (int m = 0; m < NX; ++m) u += A[m * NX + i] * G(m, jj);
-              Gn(i, jj) = u;
-            }
-          }
-          G = Gn;
-          g = gn;
-        }
         if (last) {
           NOC_UNROLL for (int i = 0; i < NX; ++i) {
             double t = g[i];
