@@ -168,7 +168,9 @@ def ipm_solve_rate(problem, N, B, rank, world, G, lo, seed=11):
     ms_all = timed(_lib.WS_NO_REPEAT_SKIP)
     U_all = eng.t["u"].clone()
     ms_index = timed(0, "index")
-    ms_cost = timed(0, "cost")
+    # the schedule "auto" replaces when the batch exceeds the resident waves (else not timed)
+    beyond = B > eng._resident_slots()
+    ms_cost = timed(0, "cost") if beyond else -1.0
     U_cost = eng.t["u"].clone()
     ms = timed(0)
     identical = bool(torch.equal(U_all, eng.t["u"])) and bool(torch.equal(U_cost, eng.t["u"]))
@@ -191,7 +193,7 @@ def ipm_solve_rate(problem, N, B, rank, world, G, lo, seed=11):
             "repeats_accounted": int(tot[4]),
             "wall_ms_recompute_all": mx[2],
             "wall_ms_index_order": mx[3],
-            "wall_ms_initial_cost_order": mx[4],
+            "wall_ms_initial_cost_order": mx[4] if mx[4] >= 0 else None,
             "schedule": "when the batch exceeds the resident waves: a probe launch of every "
                         "trajectory's first BatchedIPM.PROBE_SOLVES KKT solves, then the rest "
                         "resumed by descending total cost (timed inside wall_ms)",
