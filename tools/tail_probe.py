@@ -56,7 +56,7 @@ if "prof" in os.environ.get("NOC_HIP_LIB", ""):  # per-trajectory start / end (1
                                       if r < a.B},
                 "us_per_solve_p50": float(np.median(1e3 * (end_ms - start_ms) / solves))}
 its = eng.t["total_it"].cpu().numpy()
-tag = os.environ.get("NOC_PERSIST_HEAVY", "")
+tag = os.environ.get("TAIL_TAG", os.environ.get("NOC_PERSIST_HEAVY", ""))
 tag = f"_h{tag}" if tag else ""
 np.save(os.path.join(a.out, f"{a.problem}_N{a.N}_B{a.B}{tag}_solves.npy"), solves)
 if getattr(eng, "_order", None) is not None:  # the launch order (descending initial cost)
@@ -67,4 +67,4 @@ print(json.dumps({"problem": a.problem, "N": a.N, "B": a.B, "wall_ms": ms,
                   "p50_p90_p99_p999_max": [float(v) for v in q],
                   "n_over_300": int((solves > 300).sum()), "n_over_400": int((solves > 400).sum()),
                   "argmax": int(solves.argmax()), "mean_iters": float(its.mean()),
-                  "env_wide": os.environ.get("NOC_PERSIST_WIDE"), "env_heavy": os.environ.get("NOC_PERSIST_HEAVY"), "timeline": timeline}), flush=True)
+                  "env_wide": os.environ.get("NOC_PERSIST_WIDE"), "tag": os.environ.get("TAIL_TAG", os.environ.get("NOC_PERSIST_HEAVY")), "timeline": timeline}), flush=True)
