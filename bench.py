@@ -147,7 +147,7 @@ def ipm_solve_rate(problem, N, B, rank, world, G, lo, seed=11):
     x0, u0 = problems.shard_initial_conditions(problem, N, G, lo, lo + B, seed=seed)
     eng = BatchedIPM(ocp.family, N, B, persistent=True)
     eng.load(u0, x0)
-    eng.solve(max_steps=8)  # warm-up
+    eng.solve(max_steps=eng.PROBE_SOLVES + 8)  # warm-up: both launches of the probe schedule (their kernels loaded)
 
     def timed(flags, schedule="auto"):
         eng.load(u0, x0)

@@ -169,8 +169,10 @@ class BatchedIPM:
         self.prepare(mode, terminal)
         return torch.argsort(self.t["cost"], descending=True, stable=True).to(torch.int32)
 
-    # KKT solves of the probe launch of schedule="probe" (see solve_persistent)
-    PROBE_SOLVES = 10
+    # KKT solves of the probe launch of schedule="probe" (see solve_persistent); c3 measured
+    # 36.3 / 35.7 / 35.0 / 34.5 / 34.5 / 34.4 / 34.3 ms at 6 / 10 / 16 / 24 / 32 / 40 / 56
+    # (profiles/r05/probe_order/length/)
+    PROBE_SOLVES = 32
 
     def solve_persistent(self, mode: int = _lib.MODE_PAR, terminal: Optional[int] = None,
                          bp0: float = 0.1, max_solves: int = 10 ** 7, resume: bool = False,
@@ -182,9 +184,10 @@ class BatchedIPM:
         solve left (NOC_WS_RESUME); max_solves counts the solves of both.
         schedule: "index" launches trajectory i as workgroup i; "cost" launches them by
         descending initial cost (launch_order, ws.order); "probe" runs every trajectory's first
-        PROBE_SOLVES KKT solves in one capped launch and resumes the rest ordered by descending
-        total cost at that point, which predicts the remaining solves far better than the initial
-        cost does (c3: correlation 0.86 vs 0.3; profiles/r05/probe_order/); "auto" = "probe" when
+        PROBE_SOLVES KKT solves in one capped launch (equal jobs: two even rounds at c3) and resumes
+        the rest ordered by descending total cost at that point, which predicts the remaining
+        solves far better than the initial cost does (c3: correlation 0.86-0.89 after 10-40
+        solves vs 0.3; profiles/r05/probe_order/); "auto" = "probe" when
         the batch exceeds the resident waves and this is not a resume.  Every trajectory's result
         is the same either way (independent, deterministic, and a capped-and-resumed solve equals
         an uninterrupted one bit for bit); only the schedule changes."""

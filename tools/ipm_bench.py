@@ -17,10 +17,12 @@ lanes = int(sys.argv[5]) if len(sys.argv) > 5 else 0   # 0: the batch-aware poli
 ocp = problems.make_problem(name, N)
 x0, u0 = problems.initial_conditions(name, N, B, seed=11)
 eng = BatchedIPM(ocp.family, N, B, persistent=persistent, lanes=lanes)
+if os.environ.get("PROBE_SOLVES"):  # the probe-ordered launch's probe length (A/B only)
+    eng.PROBE_SOLVES = int(os.environ["PROBE_SOLVES"])
 if os.environ.get("NOC_NO_REPEAT_SKIP") == "1":  # recompute the identical retries at the rp clip
     eng.ws.flags = _lib.WS_NO_REPEAT_SKIP
 eng.load(u0, x0)
-eng.solve(max_steps=16)   # warm-up (kernels loaded, caches)
+eng.solve(max_steps=eng.PROBE_SOLVES + 16 if persistent else 16)   # warm-up: kernels loaded (the probe and the resume instance), caches
 torch.cuda.synchronize()
 eng.load(u0, x0)
 t0 = time.perf_counter()
