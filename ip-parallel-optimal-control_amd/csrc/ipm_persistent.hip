@@ -401,7 +401,10 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         st->it = it; st->inner = inner; st->total_it = total_it; st->solves = solves;
       }
       // ---------------- KKT solve (par_Newton, P:107-124) ----------------
-      kkt_scan_wave<NX, NU, PL, false, true, 0, false>(a, b, l);
+      // HANDOFF on (phase 3 hands the chunk's first A, B to phase 4 in registers): the two-wave
+      // cart-pole instance's scratch 524 -> 560 B/lane, but the solve is bound by its workspace
+      // traffic -- c3 ipm_solve -2.4 %, c2 -1 %, bit-identical (profiles/r05/handoff_persist/)
+      kkt_scan_wave<NX, NU, PL, false, true, 0, true>(a, b, l);
       wave_fence();  // pred / feasible written by lane 0
       {
         const IpmState* st = state_slot<NX, NU>(N);
