@@ -192,8 +192,6 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         auto lin_store = [&](int j, const LinOut& o) {
           tstore<NX * NX, PL>(w.A, b, j, l, cmax, o.fx);
           tstore<NX * NU, PL>(w.B, b, j, l, cmax, o.fu);
-          tstore<NX, PL>(w.cx, b, j, l, cmax, o.cx);
-          tstore<NU, PL>(w.cu, b, j, l, cmax, o.cu);
           if (!lc_fresh) tstore<1, PL>(w.lc, b, j, l, cmax, &o.lc);
         };
         auto load_xu = [&](int k, double* x, double* u) {
@@ -297,10 +295,11 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
           // own chunk the data are a discarded duplicate (x, u clamped into the horizon)
           tload<NX * NX, PL>(w.A, b, j, l, cmax, in.A);
           tload<NX * NU, PL>(w.B, b, j, l, cmax, in.Bm);
-          tload<NX, PL>(w.cx, b, j, l, cmax, in.cx);
-          tload<NU, PL>(w.cu, b, j, l, cmax, in.cu);
           tload<1, PL>(w.lc, b, j, l, cmax, &in.lc);
           load_xu(clampk(start + j), in.x, in.u);
+          // cx, cu re-evaluated (the linearisation's values bit for bit) instead of stored and read
+          // back: a workspace round trip of nx + nu doubles per stage against one stage_grad
+          f.stage_grad(in.x, in.u, bp, in.cx, in.cu);
         };
         // LQ blocks at lambda_{k+1} (P:35-37): Q = cxx + l.fxx, R = cuu + l.fuu, M = cxu + l.fxu;
         // ru_k = cu_k + fu_k' lambda_{k+1} (P:34); then lambda_k = cx_k + fx_k' lambda_{k+1}
