@@ -584,8 +584,8 @@ struct ArgsSrc {
 // over the blocks and one exposed memory latency instead of three dependent load chains (small
 // nx with one- or two-stage chunks, c2).
 // HANDOFF: phase 3 hands the chunk's first stage (A, B) to phase 4 in registers (standalone
-// scan: −1 stage of phase 4's re-reads); off inside the persistent solver, whose register budget
-// it would push into scratch (444 -> 516 B/lane).
+// scan: −1 stage of phase 4's re-reads); also inside the persistent solver since round 5, whose
+// solve is bound by its workspace traffic (profiles/r05/handoff_persist/).
 // BIG: the instance owns a SIMD (512 registers): the combines run masked (no identity partner).
 // AB (default: the 512-register L = 32 / 64 instances, BIG, where one wave per SIMD leaves 40 KB of
 // LDS per wave): A, B of chunk slots j < a.ab_slots stay in LDS from phase 1 to phases 3 and 4
