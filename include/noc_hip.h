@@ -170,8 +170,8 @@ typedef struct noc_ipm_ws {
   double *x, *u, *x0;                  /* (Bt,N+1,nx) (Bt,N,nu) (Bt,nx)           */
   double *A, *B, *Q, *R, *M, *r, *P;   /* LQ blocks: tiled (P natural)              */
   double *cx, *cu, *lc, *lam;          /* cx, cu, lc tiled (E = nx, nu, 1); lam (Bt,N+1,nx).
-                                          cx, cu: written by the launch-per-phase driver only
-                                          (noc_ipm_solve re-evaluates them where it needs them) */
+                                          cx, cu, lam: written by the launch-per-phase driver
+                                          only (noc_ipm_solve keeps them in registers) */
   double *dx, *du, *pred, *K, *d;      /* KKT outputs (dx, du natural; K, d tiled)  */
   int *feasible;                       /* (Bt) int32                               */
   int *phase, *kkt_active, *it, *inner, *total_it, *kkt_solves; /* (Bt) int32     */

@@ -109,7 +109,6 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
     for (int i = l; i < N * NU; i += 64) U[i] = Ug[i];
     wave_fence();
   }
-  double* LAM = w.lam + (size_t)b * (N + 1) * NX;
   const double* slot = lds_slots<NX, NU, PL>(N);
 
   KKTArgs a{};
@@ -279,10 +278,11 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
           }
           G = Gn;
         }
+        // The costates stay in registers: the solve does not store lambda to the workspace (a
+        // strided 8 * nx bytes per stage and lane, c3 ipm_solve -2.7 %, profiles/r05/lam_store/)
         double lam[NX];
         shfl_down_arr<NX>(g.v, lam, 1, PL);
         if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = lamN[i];
-        if (last) gstore<NX>(LAM + (size_t)N * NX, lamN);
         double csum = 0.0, hmax = 0.0, g2s = 0.0;
         // One stage of the costate sweep fused with its LQ blocks.  `valid` = false computes on a
         // clamped duplicate stage and leaves lambda, the sums and memory untouched (selects, not
@@ -342,7 +342,6 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
             gstore<NX * NX>(w.P + (size_t)b * NX * NX, Q);
           }
           tstore<NU, PL>(w.r, b, j, l, cmax, o.rr);
-          gstore<NX>(LAM + (size_t)k * NX, o.lam);
         };
         if (pair) {  // descending pairs over the wave-uniform chunk bound; short lanes skip slots
           for (int j = cmax - 1; j >= 0; j -= 2) {
@@ -367,7 +366,6 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         }
         // lambda at the chunk start := the scan's value g (not this lane's sweep): it is exactly the
         // boundary costate the previous lane used, so every consumer of lambda_k sees one value
-        if (len > 0) gstore<NX>(LAM + (size_t)start * NX, g.v);
         {  // the __shfl_xor butterflies with VALU partners (bit-identical, small_linalg.h)
           const int ln = (int)__lane_id();
           auto add = [](double x, double y) { return x + y; };

@@ -20,7 +20,7 @@ for k in (1, 2, 3, 5, 10):
         em.step(_lib.MODE_PAR, term)
     torch.cuda.synchronize()
     diffs = {}
-    for f in ["x", "u", "P", "lam", "A", "B", "Q", "R", "M", "r", "pred", "reg", "rp", "cost", "hu"]:
+    for f in ["x", "u", "P", "A", "B", "Q", "R", "M", "r", "pred", "reg", "rp", "cost", "hu"]:
         a, b = ep.t[f].double(), em.t[f].double()
         diffs[f] = float((a - b).abs().max())
     print(k, {f: f"{v:.1e}" for f, v in diffs.items() if v > 0}, flush=True)
