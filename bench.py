@@ -212,10 +212,28 @@ def pg():
     return dist.is_available() and dist.is_initialized()
 
 
+def parse_slice(text):
+    """--slice r/W -> (r, W)"""
+    try:
+        r, w = (int(v) for v in text.split("/"))
+    except ValueError:
+        sys.exit(f"bench.py: --slice wants r/W (e.g. 3/8), got {text!r}")
+    if not (w >= 1 and 0 <= r < w):
+        sys.exit(f"bench.py: --slice {text}: need 0 <= r < W")
+    return r, w
+
+
 def rank_shard(args, world, rank):
     """(B, G, lo, scaling): this rank's trajectories lo..lo+B-1 of the global batch G.  Strong
     scaling (default): G = --global-batch split by noc.distributed.shard_bounds; weak (--batch B):
-    G = B x world, rank r owning [rB, (r+1)B)."""
+    G = B x world, rank r owning [rB, (r+1)B).  --slice r/W (one process, no process group): what
+    rank r of a W-rank strong-scaling run solves, on this one GPU -- the per-GPU work of the
+    north-star curve's W-GPU point, measured slice by slice (tools/slice_curve.py)."""
+    if getattr(args, "slice", None):
+        from noc.distributed import shard_bounds
+        r, w = parse_slice(args.slice)
+        lo, hi = shard_bounds(args.global_batch, w, r)
+        return hi - lo, args.global_batch, lo, f"slice {r}/{w} of a strong-scaling run"
     if args.batch is not None:
         return args.batch, args.batch * world, rank * args.batch, "weak"
     from noc.distributed import shard_bounds
@@ -293,6 +311,9 @@ def main():
                     help="total trajectories, split over the ranks (strong scaling; default c3)")
     ap.add_argument("--batch", type=int, default=None,
                     help="trajectories per GPU instead (weak scaling)")
+    ap.add_argument("--slice", default=None,
+                    help="r/W: solve only rank r's shard of a W-rank strong-scaling run, on one "
+                         "GPU without a process group (value then counts the slice only)")
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--layout", choices=["tiled", "natural"], default="tiled",
                     help="HBM layout of the LQ blocks (tiled = what the linearisation kernels write)")
@@ -313,6 +334,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.slice and (args.gpus != 1 or args.batch is not None):
+        sys.exit("bench.py: --slice runs one process on one GPU (--gpus 1) of the strong-scaling "
+                 "global batch (no --batch)")
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} "
                  f"ranks; refusing to report a line whose n_gpus would not be what was asked")
@@ -413,7 +437,9 @@ def main():
         rank_kern_ms = allgather_float(kern_ms)
         ms, kern_ms = allreduce([ms, kern_ms], "max")
     feasible_frac = float(out.feasible.float().mean())
-    value = G * args.steps / (ms * args.steps / 1e3)
+    # trajectories this run solved per step: the global batch (every rank's shard), or one slice
+    solved = B if args.slice else G
+    value = solved * args.steps / (ms * args.steps / 1e3)
     abytes = algorithmic_bytes(nx, nu, N, B)
     if pg():  # the slowest rank's bytes (shards differ by at most one trajectory)
         abytes = int(allreduce([abytes], "max")[0])
@@ -462,7 +488,11 @@ def main():
         "per_rank_kernel_ms": rank_kern_ms,
         "feasible_fraction": feasible_frac,
         "launch": "eager" if graph is None else "hip_graph (the K timed steps captured once, one replay)",
+        "build_hash": _lib.load().noc_build_hash().decode(),  # == the tree's (checked by load())
     }
+    if args.slice:
+        result["config"]["slice"] = args.slice
+        result["config"]["slice_trajectories"] = [lo, lo + B]
     if not args.no_ipm:
         result["ipm_solve"] = ipm_solve_rate(args.problem, N, B, rank, world, G, lo)
     if rank == 0 and world == 1 and not args.no_cpu:

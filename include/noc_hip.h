@@ -42,6 +42,11 @@ extern "C" {
 
 /* Library identity / diagnostics. */
 int noc_abi_version(void);
+/* Provenance of the binary: the first 16 hex digits of sha256 over the sources it was compiled
+ * from (the .hip, .h and .def files of csrc/ and csrc/custom/ in name order, then this header), baked in by
+ * the Makefile.  The Python host refuses a library whose hash differs from the tree's
+ * (noc/_lib.py: load), so a stale binary cannot pass for the current sources. */
+const char* noc_build_hash(void);
 const char* noc_last_error(void);
 int noc_kkt_supported(int nx, int nu);
 /* Lanes per trajectory used when a solve is called with lanes = 0 (batch-agnostic). */

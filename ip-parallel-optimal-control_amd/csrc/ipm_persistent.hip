@@ -19,6 +19,7 @@
 #include <cstdlib>
 
 #include "../../include/noc_hip.h"
+#include "block_struct.h"
 #include "ipm_family.h"
 #include "kkt_scan_impl.h"
 #include "noc_internal.h"
@@ -65,6 +66,54 @@ NOC_DEV constexpr int xlds_off(int N) {
 template <int NX, int NU>
 NOC_DEV constexpr int xlds_doubles(int N) { return ((N + 1) * NX + N * NU + 1) & ~1; }
 
+// The KKT scan's block source in the persistent solver: the workspace's compact tiled fields (only
+// the variable entries of A, B, Q, R, M; block_struct.h), expanded with the family's constants as
+// they are loaded.  BS = BlockStruct<..., false> is the dense layout (the NOC_PERSIST_STRUCT=0
+// instance), which loads exactly what ArgsSrc does.
+template <class BS, int NX, int NU, int L>
+struct CompactSrc {
+  using Struct = BS;
+  const KKTArgs& a;
+  const noc_family& p;
+  int traj, l, cmax;
+  size_t tN;
+  template <int F, bool LAST = false>
+  NOC_DEV void field(const double* base, int j, double* full) const {
+    constexpr int EV = BS::template nv<F>();
+    double v[EV > 0 ? EV : 1];
+    if constexpr (EV > 0) tload_pol<EV, L, LAST>(base, traj, j, l, cmax, v);
+    BS::template expand<F>(p, v, full);
+  }
+  // PART / LAST: as load_stage (kkt_scan_impl.h)
+  template <int PART, bool LAST = false>
+  NOC_DEV void stage_part(int s, int j, double reg, StageData<NX, NU>& st) const {
+    constexpr bool REST = PART != 2, WQ = PART != 1, WAB = REST && PART != 3;
+    (void)s;
+    (void)reg;
+    if constexpr (WAB) {
+      field<BF_A>(a.A, j, st.A.v);
+      field<BF_B>(a.Bm, j, st.B.v);
+    }
+    if constexpr (WQ) field<BF_Q, LAST>(a.Q, j, st.Q.v);
+    if constexpr (REST) {
+      field<BF_R, LAST>(a.R, j, st.R.v);
+      field<BF_M, LAST>(a.M, j, st.M.v);
+      tload_pol<NU, L, LAST>(a.r, traj, j, l, cmax, st.r.v);
+    }
+  }
+  NOC_DEV void stage(int s, int j, double reg, StageData<NX, NU>& st) const { stage_part<0>(s, j, reg, st); }
+  NOC_DEV void stage_last(int s, int j, double reg, StageData<NX, NU>& st) const {
+    stage_part<0, true>(s, j, reg, st);
+  }
+  NOC_DEV void ab(int s, int j, Mat<NX, NX>& A, Mat<NX, NU>& Bm, Vec<NX>& c) const {
+    (void)s;
+    field<BF_A, true>(a.A, j, A.v);  // phase 4: the last read of A, B (non-temporal)
+    field<BF_B, true>(a.Bm, j, Bm.v);
+    set_zero(c);
+  }
+  NOC_DEV void cvec(int, int, Vec<NX>& c) const { set_zero(c); }
+};
+
 }  // namespace
 
 #ifdef NOC_PERSIST_PROFILE
@@ -78,7 +127,9 @@ NOC_DEV constexpr int xlds_doubles(int N) { return ((N + 1) * NX + N * NU + 1) &
 // of scratch per lane at WPS = 2, none at WPS = 1), and which pays for the stage pairs below.
 // RESUME: continue from the workspace state (NOC_WS_RESUME; its own instance, so the plain solve's
 // register allocation does not carry the resume bookkeeping).
-template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS>
+// STRUCT: the structure-aware blocks (block_struct.h; NOC_PERSIST_STRUCT=0 selects the dense
+// instance, which computes the same doubles).
+template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS, bool STRUCT>
 __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
                                                          int terminal, double bp0,
                                                          int max_solves) {
@@ -88,6 +139,9 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
   if (b < 0 || b >= w.Bt) return;  // an out-of-range order entry solves nothing (never faults)
   constexpr int KD = kd_width<NX, NU>();
   Fam<KIND, NX, NU> f(prm);
+  using BS = BlockStruct<KIND, NX, NU, STRUCT>;
+  constexpr int VA = BS::template nv<BF_A>(), VB = BS::template nv<BF_B>();
+  constexpr int VQ = BS::template nv<BF_Q>(), VR = BS::template nv<BF_R>(), VM = BS::template nv<BF_M>();
   const int N = w.N;
   const Chunks ch(N, PL);
   const int start = ch.start(l), len = ch.len(l), cmax = ch.cmax;
@@ -174,7 +228,12 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
     wave_fence();  // states of every stage visible to their chunk owners
     NOC_PHASE(0);
     lc_fresh = false;
-    bool relinearize = !RESUME || entry != NOC_PHASE_SOLVE;  // SOLVE: the ws blocks are current
+    // A SOLVE resume (a retry on the current point) recomputes the blocks from the workspace's
+    // states -- the same doubles the capped launch had; the workspace blocks may be another
+    // driver's layout (dense / compact) -- and keeps the solver state it left (cost, |Hu|,
+    // ||cu||, the retry counter), like the wide kernel (ipm_wide.hip)
+    bool relinearize = true;
+    bool keep_state = RESUME && entry == NOC_PHASE_SOLVE;
     if constexpr (RESUME) entry = NOC_PHASE_ROLLOUT;
     bool stage_done = false;
     while (!stage_done) {  // ---------------- Newton iterations (P:127-225) ----------------
@@ -185,12 +244,17 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         };
         auto lin_compute = [&](const double* x, const double* u, LinOut& o) {
           f.jac(x, u, o.fx, o.fu);
+          BS::template fold_consts<BF_A>(prm, o.fx);  // structural entries as literals / parameters
+          BS::template fold_consts<BF_B>(prm, o.fu);
           f.stage_grad(x, u, bp, o.cx, o.cu);
           if (!lc_fresh) o.lc = f.stage_cost(x, u, bp);  // uniform over the wave
         };
-        auto lin_store = [&](int j, const LinOut& o) {
-          tstore<NX * NX, PL>(w.A, b, j, l, cmax, o.fx);
-          tstore<NX * NU, PL>(w.B, b, j, l, cmax, o.fu);
+        auto lin_store = [&](int j, const LinOut& o) {  // compact A, B: variable entries only
+          double va[VA > 0 ? VA : 1], vb[VB > 0 ? VB : 1];
+          BS::template compress<BF_A>(o.fx, va);
+          BS::template compress<BF_B>(o.fu, vb);
+          if constexpr (VA > 0) tstore<VA, PL>(w.A, b, j, l, cmax, va);
+          if constexpr (VB > 0) tstore<VB, PL>(w.B, b, j, l, cmax, vb);
           if (!lc_fresh) tstore<1, PL>(w.lc, b, j, l, cmax, &o.lc);
         };
         auto load_xu = [&](int k, double* x, double* u) {
@@ -211,11 +275,11 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
           Vec<NX> gn;
           NOC_UNROLL for (int i = 0; i < NX; ++i) {
             double t = o.cx[i];
-            NOC_UNROLL for (int m = 0; m < NX; ++m) t += o.fx[m * NX + i] * g[m];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) if (BS::nzA(m, i)) t += o.fx[m * NX + i] * g[m];
             gn[i] = t;
             NOC_UNROLL for (int jj = 0; jj < NX; ++jj) {
               double u = 0.0;
-              NOC_UNROLL for (int m = 0; m < NX; ++m) u += o.fx[m * NX + i] * G(m, jj);
+              NOC_UNROLL for (int m = 0; m < NX; ++m) if (BS::nzA(m, i)) u += o.fx[m * NX + i] * G(m, jj);
               Gn(i, jj) = u;
             }
           }
@@ -293,8 +357,11 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         auto load_in = [&](int j, StageIn& in) {
           // 0 <= j < cmax: every lane's tiled slots exist up to cmax; for a slot past the lane's
           // own chunk the data are a discarded duplicate (x, u clamped into the horizon)
-          tload<NX * NX, PL>(w.A, b, j, l, cmax, in.A);
-          tload<NX * NU, PL>(w.B, b, j, l, cmax, in.Bm);
+          double va[VA > 0 ? VA : 1], vb[VB > 0 ? VB : 1];
+          if constexpr (VA > 0) tload<VA, PL>(w.A, b, j, l, cmax, va);
+          if constexpr (VB > 0) tload<VB, PL>(w.B, b, j, l, cmax, vb);
+          BS::template expand<BF_A>(prm, va, in.A);
+          BS::template expand<BF_B>(prm, vb, in.Bm);
           tload<1, PL>(w.lc, b, j, l, cmax, &in.lc);
           load_xu(clampk(start + j), in.x, in.u);
           // cx, cu re-evaluated (the linearisation's values bit for bit) instead of stored and read
@@ -312,20 +379,23 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
           double Q[NX * NX], R[NU * NU];
           f.stage_hess(in.x, in.u, bp, Q, R, o.M);
           f.add_hess_l(in.x, in.u, lam, Q, R, o.M);
+          BS::template fold_consts<BF_M>(prm, o.M);
           NOC_UNROLL for (int i = 0; i < NX; ++i)
             NOC_UNROLL for (int jj = i; jj < NX; ++jj) o.Qs(i, jj) = (i == jj) ? Q[i * NX + i] : 0.5 * (Q[i * NX + jj] + Q[jj * NX + i]);
           NOC_UNROLL for (int i = 0; i < NU; ++i)
             NOC_UNROLL for (int jj = i; jj < NU; ++jj) o.Rs(i, jj) = (i == jj) ? R[i * NU + i] : 0.5 * (R[i * NU + jj] + R[jj * NU + i]);
+          BS::template fold_consts<BF_Q>(prm, o.Qs.v);
+          BS::template fold_consts<BF_R>(prm, o.Rs.v);
           NOC_UNROLL for (int jj = 0; jj < NU; ++jj) {
             double r = in.cu[jj];
-            NOC_UNROLL for (int i = 0; i < NX; ++i) r += in.Bm[i * NU + jj] * lam[i];
+            NOC_UNROLL for (int i = 0; i < NX; ++i) if (BS::nzB(i, jj)) r += in.Bm[i * NU + jj] * lam[i];
             o.rr[jj] = r;
             hmax = valid ? nan_max(hmax, fabs(r)) : hmax;
             g2s = valid ? g2s + in.cu[jj] * in.cu[jj] : g2s;
           }
           NOC_UNROLL for (int i = 0; i < NX; ++i) {
             double t = in.cx[i];
-            NOC_UNROLL for (int m = 0; m < NX; ++m) t += in.A[m * NX + i] * lam[m];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) if (BS::nzA(m, i)) t += in.A[m * NX + i] * lam[m];
             o.lam[i] = t;
           }
           csum = valid ? csum + in.lc : csum;
@@ -333,9 +403,13 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         };
         auto cost_store = [&](int j, const StageIn& in, const StageOut& o) {
           const int k = start + j;
-          tstore<Sym<NX>::SZ, PL>(w.Q, b, j, l, cmax, o.Qs.v);
-          tstore<Sym<NU>::SZ, PL>(w.R, b, j, l, cmax, o.Rs.v);
-          tstore<NX * NU, PL>(w.M, b, j, l, cmax, o.M);
+          double vq[VQ > 0 ? VQ : 1], vr[VR > 0 ? VR : 1], vm[VM > 0 ? VM : 1];
+          BS::template compress<BF_Q>(o.Qs.v, vq);
+          BS::template compress<BF_R>(o.Rs.v, vr);
+          BS::template compress<BF_M>(o.M, vm);
+          if constexpr (VQ > 0) tstore<VQ, PL>(w.Q, b, j, l, cmax, vq);
+          if constexpr (VR > 0) tstore<VR, PL>(w.R, b, j, l, cmax, vr);
+          if constexpr (VM > 0) tstore<VM, PL>(w.M, b, j, l, cmax, vm);
           if (terminal == NOC_TERMINAL_STAGE0 && k == 0) {  // XT = Q[0] (P:73), full matrix
             double Q[NX * NX];
             NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int jj = 0; jj < NX; ++jj) Q[i * NX + jj] = o.Qs(i, jj);
@@ -378,11 +452,14 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
           f.final_hess(xN, P);
           gstore<NX * NX>(w.P + (size_t)b * NX * NX, P);
         }
-        // total_cost(x, u, bp) (P:142); x_N is the last lane's own (trial) store
-        cost = readlane_d(csum + f.final_cost(xN), PL - 1);
-        hu = hmax;                                        // max |Hu| (P:158)
-        gnorm = sqrt(g2s);                                // ||cu||_F (P:116)
-        inner = 0;
+        if (!keep_state) {
+          // total_cost(x, u, bp) (P:142); x_N is the last lane's own (trial) store
+          cost = readlane_d(csum + f.final_cost(xN), PL - 1);
+          hu = hmax;                                      // max |Hu| (P:158)
+          gnorm = sqrt(g2s);                              // ||cu||_F (P:116)
+          inner = 0;
+        }
+        keep_state = false;
         // regularisation: par R += rp*||cu||*I (P:116-118); seq Quu += mu*I (S:51)
         const double reg = (mode == NOC_MODE_PAR) ? rp * gnorm : rp;
         w.reg[b] = reg;  // every lane stores the same value and reads its own store back
@@ -401,7 +478,10 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       // HANDOFF on (phase 3 hands the chunk's first A, B to phase 4 in registers): the two-wave
       // cart-pole instance's scratch 524 -> 560 B/lane, but the solve is bound by its workspace
       // traffic -- c3 ipm_solve -2.4 %, c2 -1 %, bit-identical (profiles/r05/handoff_persist/)
-      kkt_scan_wave<NX, NU, PL, false, true, 0, true>(a, b, l);
+      {
+        const CompactSrc<BS, NX, NU, PL> src{a, prm, b, l, cmax, (size_t)b * N};
+        kkt_scan_wave_src<NX, NU, PL, false, true, CompactSrc<BS, NX, NU, PL>, 0, true>(a, b, l, src);
+      }
       wave_fence();  // pred / feasible written by lane 0
       {
         const IpmState* st = state_slot<NX, NU>(N);
@@ -566,8 +646,14 @@ constexpr bool one_wave_instance() { return KIND == NOC_FAMILY_CARTPOLE; }
 template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS>
 static hipError_t launch_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                                double bp0, int max_solves, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, WPS, RESUME, XLDS>), dim3(w.Bt), dim3(64),
-                     lds, s, p, w, mode, terminal, bp0, max_solves);
+  // the structure-aware blocks unless NOC_PERSIST_STRUCT=0 (per launch: tests switch it)
+  const char* senv = getenv("NOC_PERSIST_STRUCT");
+  if (senv && atoi(senv) == 0)
+    hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, WPS, RESUME, XLDS, false>), dim3(w.Bt), dim3(64),
+                       lds, s, p, w, mode, terminal, bp0, max_solves);
+  else
+    hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, WPS, RESUME, XLDS, true>), dim3(w.Bt), dim3(64),
+                       lds, s, p, w, mode, terminal, bp0, max_solves);
   return hipGetLastError();
 }
 

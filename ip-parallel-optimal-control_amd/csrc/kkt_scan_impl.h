@@ -59,6 +59,15 @@ __device__ long long g_scan_stamps[kStampWaves][kStampSlots][2];
 #define NOC_STAMP(i) do { } while (0)
 #endif
 
+// Which entries of a stage's A, B may be nonzero: the generic scan takes every one; the persistent
+// solver's structure-aware blocks (block_struct.h: BlockStruct) skip the products with structural
+// zeros.  nzA / nzB are called with unrolled (compile-time) indices.
+template <int NX, int NU>
+struct DenseBlocks {
+  static constexpr bool nzA(int, int) { return true; }
+  static constexpr bool nzB(int, int) { return true; }
+};
+
 template <int NX, int NU>
 struct StageData {
   Mat<NX, NX> A;
@@ -177,19 +186,19 @@ NOC_DEV void load_Kd(const KKTArgs& a, int traj, size_t si, int j, int l, int cm
 }
 
 // e <- stage (x) e   (Riccati-form prepend of one stage to the chunk element)
-template <int NX, int NU, bool AFF>
+template <int NX, int NU, bool AFF, class ST = DenseBlocks<NX, NU>>
 NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st, double reg) {
   Mat<NX, NX> JA;
   Mat<NX, NU> JB;
   NOC_UNROLL for (int i = 0; i < NX; ++i) {
     NOC_UNROLL for (int j = 0; j < NX; ++j) {
       double s = 0.0;
-      NOC_UNROLL for (int k = 0; k < NX; ++k) s += e.J(i, k) * st.A(k, j);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzA(k, j)) s += e.J(i, k) * st.A(k, j);
       JA(i, j) = s;
     }
     NOC_UNROLL for (int j = 0; j < NU; ++j) {
       double s = 0.0;
-      NOC_UNROLL for (int k = 0; k < NX; ++k) s += e.J(i, k) * st.B(k, j);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzB(k, j)) s += e.J(i, k) * st.B(k, j);
       JB(i, j) = s;
     }
   }
@@ -203,7 +212,7 @@ NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st, double reg) {
   NOC_UNROLL for (int i = 0; i < NU; ++i)
     NOC_UNROLL for (int j = i; j < NU; ++j) {
       double s = (i == j) ? st.R(i, j) + reg : st.R(i, j);  // R + reg I (P:116-118)
-      NOC_UNROLL for (int k = 0; k < NX; ++k) s += st.B(k, i) * JB(k, j);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzB(k, i)) s += st.B(k, i) * JB(k, j);
       W(i, j) = s;
     }
   // AB = e.A * B
@@ -211,7 +220,7 @@ NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st, double reg) {
   NOC_UNROLL for (int i = 0; i < NX; ++i)
     NOC_UNROLL for (int j = 0; j < NU; ++j) {
       double s = 0.0;
-      NOC_UNROLL for (int k = 0; k < NX; ++k) s += e.A(i, k) * st.B(k, j);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzB(k, j)) s += e.A(i, k) * st.B(k, j);
       AB(i, j) = s;
     }
   // Y = [Qux | Qu | AB']  (NU x (2NX+1))
@@ -221,12 +230,12 @@ NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st, double reg) {
   NOC_UNROLL for (int i = 0; i < NU; ++i) {
     NOC_UNROLL for (int j = 0; j < NX; ++j) {
       double s = st.M(j, i);
-      NOC_UNROLL for (int k = 0; k < NX; ++k) s += JB(k, i) * st.A(k, j);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzA(k, j)) s += JB(k, i) * st.A(k, j);
       Qux(i, j) = s;
       Y[i][j] = s;
     }
     double s = st.r[i];
-    NOC_UNROLL for (int k = 0; k < NX; ++k) s += st.B(k, i) * g[k];
+    NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzB(k, i)) s += st.B(k, i) * g[k];
     Y[i][NX] = s;
     NOC_UNROLL for (int t = 0; t < NX; ++t) Y[i][NX + 1 + t] = AB(t, i);
   }
@@ -236,13 +245,13 @@ NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st, double reg) {
   NOC_UNROLL for (int i = 0; i < NX; ++i)
     NOC_UNROLL for (int j = i; j < NX; ++j) {
       double s = st.Q(i, j);
-      NOC_UNROLL for (int k = 0; k < NX; ++k) s += st.A(k, i) * JA(k, j);
+      NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzA(k, i)) s += st.A(k, i) * JA(k, j);
       NOC_UNROLL for (int t = 0; t < NU; ++t) s -= Qux(t, i) * Y[t][j];
       Jn(i, j) = s;
     }
   NOC_UNROLL for (int i = 0; i < NX; ++i) {
     double s = AFF ? st.q[i] : 0.0;
-    NOC_UNROLL for (int k = 0; k < NX; ++k) s += st.A(k, i) * g[k];
+    NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzA(k, i)) s += st.A(k, i) * g[k];
     NOC_UNROLL for (int t = 0; t < NU; ++t) s -= Qux(t, i) * Y[t][NX];
     e.nu[i] = s;
   }
@@ -260,11 +269,11 @@ NOC_DEV void prepend(Elem<NX>& e, const StageData<NX, NU>& st, double reg) {
   NOC_UNROLL for (int i = 0; i < NX; ++i) {
     NOC_UNROLL for (int j = 0; j < NX; ++j) {
       double s = st.A(i, j);
-      NOC_UNROLL for (int t = 0; t < NU; ++t) s -= st.B(i, t) * Y[t][j];
+      NOC_UNROLL for (int t = 0; t < NU; ++t) if (ST::nzB(i, t)) s -= st.B(i, t) * Y[t][j];
       F(i, j) = s;
     }
     double s = AFF ? st.c[i] : 0.0;
-    NOC_UNROLL for (int t = 0; t < NU; ++t) s -= st.B(i, t) * Y[t][NX];
+    NOC_UNROLL for (int t = 0; t < NU; ++t) if (ST::nzB(i, t)) s -= st.B(i, t) * Y[t][NX];
     f[i] = s;
   }
   Mat<NX, NX> An;
@@ -554,6 +563,7 @@ NOC_DEV void apply_value(Elem<NX>& e1, const Sym<NX>& J2, const Vec<NX>& nu2) {
 // The persistent solver passes a source that recomputes them from (x, u, lambda) instead.
 template <int NX, int NU, int L, bool AFF, bool TILED>
 struct ArgsSrc {
+  using Struct = DenseBlocks<NX, NU>;
   const KKTArgs& a;
   int traj, l, cmax;
   size_t tN;
@@ -595,6 +605,7 @@ template <int NX, int NU, int L, bool AFF, bool TILED, class SRC, int CACHE = 0,
           bool BIG = false, bool NT3 = false, bool AB = (BIG && ab_supported<NX, NU>())>
 NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, const SRC& src) {
   constexpr int KD = kd_width<NX, NU>();
+  using ST = typename SRC::Struct;  // structural zeros of A, B (DenseBlocks: none)
   if (traj >= a.B) return;                     // uniform over the segment
   if (a.active && a.active[traj] == 0) return;  // uniform over the segment
   const int N = a.N;
@@ -664,13 +675,13 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     }
     if constexpr (CACHE > 0) {
       NOC_UNROLL for (int jj = CACHE - 1; jj >= 0; --jj)
-        if (jj < len) prepend<NX, NU, AFF>(e, cache[jj], reg);
+        if (jj < len) prepend<NX, NU, AFF, ST>(e, cache[jj], reg);
     } else {
       for (int s = start + len - 1; s >= start; --s) {
         StageData<NX, NU> st;
         src.stage(s, s - start, reg, st);
         if constexpr (AB) { if (s - start < abn) ab_store<NX, NU>(lab, s - start, st.A, st.B); }
-        prepend<NX, NU, AFF>(e, st, reg);
+        prepend<NX, NU, AFF, ST>(e, st, reg);
       }
     }
     NOC_STAMP(1); NOC_ISA_MARK("phase", 1);
@@ -743,12 +754,12 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       NOC_UNROLL for (int i = 0; i < NX; ++i) {
         NOC_UNROLL for (int j = 0; j < NX; ++j) {
           double t = 0.0;
-          NOC_UNROLL for (int k = 0; k < NX; ++k) t += S(i, k) * st.A(k, j);
+          NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzA(k, j)) t += S(i, k) * st.A(k, j);
           SA(i, j) = t;
         }
         NOC_UNROLL for (int j = 0; j < NU; ++j) {
           double t = 0.0;
-          NOC_UNROLL for (int k = 0; k < NX; ++k) t += S(i, k) * st.B(k, j);
+          NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzB(k, j)) t += S(i, k) * st.B(k, j);
           SB(i, j) = t;
         }
       }
@@ -762,7 +773,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       NOC_UNROLL for (int i = 0; i < NU; ++i)
         NOC_UNROLL for (int j = i; j < NU; ++j) {
           double t = (i == j) ? st.R(i, j) + reg : st.R(i, j);  // R + reg I (P:116-118)
-          NOC_UNROLL for (int k = 0; k < NX; ++k) t += st.B(k, i) * SB(k, j);
+          NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzB(k, i)) t += st.B(k, i) * SB(k, j);
           Quu(i, j) = t;
         }
       constexpr int NR = NX + 1;
@@ -772,12 +783,12 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       NOC_UNROLL for (int i = 0; i < NU; ++i) {
         NOC_UNROLL for (int j = 0; j < NX; ++j) {
           double t = st.M(j, i);
-          NOC_UNROLL for (int k = 0; k < NX; ++k) t += SB(k, i) * st.A(k, j);
+          NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzA(k, j)) t += SB(k, i) * st.A(k, j);
           Qux(i, j) = t;
           Y[i][j] = t;
         }
         double t = st.r[i];
-        NOC_UNROLL for (int k = 0; k < NX; ++k) t += st.B(k, i) * g[k];
+        NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzB(k, i)) t += st.B(k, i) * g[k];
         Qu[i] = t;
         Y[i][NX] = t;
       }
@@ -804,13 +815,13 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       NOC_UNROLL for (int i = 0; i < NX; ++i)
         NOC_UNROLL for (int j = i; j < NX; ++j) {
           double t = st.Q(i, j);
-          NOC_UNROLL for (int k = 0; k < NX; ++k) t += st.A(k, i) * SA(k, j);
+          NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzA(k, i)) t += st.A(k, i) * SA(k, j);
           NOC_UNROLL for (int u = 0; u < NU; ++u) t += Qux(u, i) * Kk[u * NX + j];
           Sn(i, j) = t;
         }
       NOC_UNROLL for (int i = 0; i < NX; ++i) {
         double t = AFF ? st.q[i] : 0.0;
-        NOC_UNROLL for (int k = 0; k < NX; ++k) t += st.A(k, i) * g[k];
+        NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzA(k, i)) t += st.A(k, i) * g[k];
         NOC_UNROLL for (int u = 0; u < NU; ++u) t += Qux(u, i) * Kk[NU * NX + u];
         v[i] = t;
       }
@@ -823,11 +834,11 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       NOC_UNROLL for (int i = 0; i < NX; ++i) {
         NOC_UNROLL for (int j = 0; j < NX; ++j) {
           double t = st.A(i, j);
-          NOC_UNROLL for (int u = 0; u < NU; ++u) t += st.B(i, u) * Kk[u * NX + j];
+          NOC_UNROLL for (int u = 0; u < NU; ++u) if (ST::nzB(i, u)) t += st.B(i, u) * Kk[u * NX + j];
           F(i, j) = t;
         }
         double t = AFF ? st.c[i] : 0.0;
-        NOC_UNROLL for (int u = 0; u < NU; ++u) t += st.B(i, u) * Kk[NU * NX + u];
+        NOC_UNROLL for (int u = 0; u < NU; ++u) if (ST::nzB(i, u)) t += st.B(i, u) * Kk[NU * NX + u];
         f[i] = t;
       }
       Mat<NX, NX> Pn;
@@ -928,11 +939,11 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       NOC_UNROLL for (int i = 0; i < NX; ++i) {
         NOC_UNROLL for (int j = 0; j < NX; ++j) {
           double t = A(i, j);
-          NOC_UNROLL for (int u = 0; u < NU; ++u) t += Bm(i, u) * Kk[u * NX + j];
+          NOC_UNROLL for (int u = 0; u < NU; ++u) if (ST::nzB(i, u)) t += Bm(i, u) * Kk[u * NX + j];
           F(i, j) = t;
         }
         double t = cc[i];
-        NOC_UNROLL for (int u = 0; u < NU; ++u) t += Bm(i, u) * Kk[NU * NX + u];
+        NOC_UNROLL for (int u = 0; u < NU; ++u) if (ST::nzB(i, u)) t += Bm(i, u) * Kk[NU * NX + u];
         f[i] = t;
       }
       Mat<NX, NX> Pn;
@@ -1025,8 +1036,8 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     Vec<NX> xn;
     NOC_UNROLL for (int i = 0; i < NX; ++i) {
       double t = cc[i];
-      NOC_UNROLL for (int k = 0; k < NX; ++k) t += A(i, k) * x[k];
-      NOC_UNROLL for (int j = 0; j < NU; ++j) t += Bm(i, j) * u[j];
+      NOC_UNROLL for (int k = 0; k < NX; ++k) if (ST::nzA(i, k)) t += A(i, k) * x[k];
+      NOC_UNROLL for (int j = 0; j < NU; ++j) if (ST::nzB(i, j)) t += Bm(i, j) * u[j];
       xn[i] = t;
     }
     x = xn;

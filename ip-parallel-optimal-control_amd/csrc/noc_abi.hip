@@ -109,9 +109,15 @@ int kkt_pick_lanes(int nx, int nu, int N, int B) {
 }
 }  // namespace noc
 
+// sha256 (16 hex digits) of the sources, from the Makefile (-DNOC_BUILD_HASH); include/noc_hip.h
+#ifndef NOC_BUILD_HASH
+#define NOC_BUILD_HASH "unknown"
+#endif
+
 extern "C" {
 
 int noc_abi_version(void) { return NOC_ABI_VERSION; }
+const char* noc_build_hash(void) { return NOC_BUILD_HASH; }
 void noc_debug_set_ablation(int bits) { g_ablate = bits; }
 const char* noc_last_error(void) { return g_last_error.c_str(); }
 int noc_kkt_supported(int nx, int nu) { return noc::kkt_supported(nx, nu) ? 1 : 0; }

@@ -121,7 +121,25 @@ def emit(name, X, U, f):
     block(f"NOC_DEV void {name}_ode_hess_l(const double* x, const double* u, const double* l, double* H)",
           [hl[a][b] for a in range(nz) for b in range(nz)],
           [f"H[{a * nz + b}]" for a in range(nz) for b in range(nz)], with_lambda=True)
+    lines.append(structure(name, "jac", [jac[i][j] for i in range(nx) for j in range(nz)], Z))
+    lines.append(f"constexpr signed char {name}_hess_nz[{nz * nz}] = "
+                 f"{{{', '.join('0' if hl[a][b] == 0 else '1' for a in range(nz) for b in range(nz))}}};")
     return "\n".join(lines)
+
+
+def structure(name, what, exprs, args) -> str:
+    """The structural pattern of a generated array (csrc/block_struct.h): {name}_{what}_var[k] = 1
+    where entry k depends on the arguments, else 0 with its value in {name}_{what}_const[k] -- the
+    very literal the device function assigns, so a kernel that folds it in computes the same
+    doubles as one that evaluates the function.  A constant that is not a plain number (pi,
+    sqrt(2), ...) counts as variable."""
+    args = set(args)
+    var = [not (sp.sympify(e).is_Number and not (sp.sympify(e).free_symbols & args)) for e in exprs]
+    vals = ["0" if v else _ccode(sp.sympify(e)) for v, e in zip(var, exprs)]
+    n = len(exprs)
+    return "\n".join([
+        f"constexpr signed char {name}_{what}_var[{n}] = {{{', '.join('1' if v else '0' for v in var)}}};",
+        f"constexpr double {name}_{what}_const[{n}] = {{{', '.join(vals)}}};"])
 
 
 # numpy ufunc name -> sympy function: numpy applies a ufunc to an object array (or a sympy scalar)
@@ -220,6 +238,7 @@ def emit_costs(name, X, U, bp, stage, final, cons):
            [f"H[{k}]" for k in range(nx * nx)], X, [])
     _block(lines, f"NOC_DEV bool {name}_feasible(const double* x, const double* u)",
            list(cons), [], X, U, ret="all_nonpositive")
+    lines.append(structure(name, "cost_hess", Q + R + M, list(X) + list(U) + [bp]))
     return "\n".join(lines)
 
 

@@ -32,6 +32,7 @@ _i = ctypes.c_int
 # name -> (restype, argtypes); mirrors include/noc_hip.h exactly (tests check every symbol)
 SIGNATURES = {
     "noc_abi_version": (_i, []),
+    "noc_build_hash": (ctypes.c_char_p, []),
     "noc_last_error": (ctypes.c_char_p, []),
     "noc_kkt_supported": (_i, [_i, _i]),
     "noc_kkt_default_lanes": (_i, [_i, _i, _i]),
@@ -121,18 +122,50 @@ class NocError(RuntimeError):
     pass
 
 
-def _typed(lib: ctypes.CDLL) -> ctypes.CDLL:
+def tree_build_hash(pkg_root: Optional[str] = None) -> str:
+    """sha256 (16 hex digits) of the sources in this tree that libnoc_hip.so is compiled from --
+    csrc/*.hip, *.h, *.def and csrc/custom/*.hip in name order, then include/noc_hip.h -- the same
+    bytes the Makefile hashes into noc_build_hash()."""
+    import glob
+    import hashlib
+    pkg = pkg_root or os.path.dirname(_HERE)
+    rel = sorted(os.path.relpath(f, pkg) for pat in ("csrc/*.hip", "csrc/*.h", "csrc/*.def",
+                                                     "csrc/custom/*.hip")
+                 for f in glob.glob(os.path.join(pkg, pat)))
+    h = hashlib.sha256()
+    for f in rel + [os.path.join("..", "include", "noc_hip.h")]:
+        with open(os.path.join(pkg, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def verify_build(lib: ctypes.CDLL, pkg_root: Optional[str] = None) -> str:
+    """The library's baked-in source hash; NocError if it is not this tree's (a stale binary).
+    NOC_ALLOW_STALE_LIB=1 downgrades the refusal (development only: an edited source that is not
+    rebuilt yet)."""
+    built = lib.noc_build_hash().decode()
+    tree = tree_build_hash(pkg_root)
+    if built != tree and os.environ.get("NOC_ALLOW_STALE_LIB") != "1":
+        raise NocError(f"{getattr(lib, '_name', 'libnoc_hip.so')} was built from other sources "
+                       f"(library {built}, tree {tree}); rebuild it: "
+                       f"`make -C ip-parallel-optimal-control_amd -j8`")
+    return built
+
+
+def _typed(lib: ctypes.CDLL, pkg_root: Optional[str] = None) -> ctypes.CDLL:
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     if lib.noc_abi_version() != ABI_VERSION:
         raise NocError("libnoc_hip.so ABI version mismatch")
+    verify_build(lib, pkg_root)
     return lib
 
 
-def load(path: Optional[str] = None) -> ctypes.CDLL:
-    """Load (once) and type the shared library.  Raises NocError if it is missing."""
+def load(path: Optional[str] = None, pkg_root: Optional[str] = None) -> ctypes.CDLL:
+    """Load (once) and type the shared library.  Raises NocError if it is missing or was built
+    from other sources than this tree's (verify_build; pkg_root: the tree to check against)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -140,7 +173,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     if not os.path.exists(p):
         raise NocError(f"libnoc_hip.so not found at {p}; build it with "
                        f"`make -C ip-parallel-optimal-control_amd -j8`")
-    lib = _typed(ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL))
+    lib = _typed(ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL), pkg_root)
     if path is None:
         _lib = lib
     return lib

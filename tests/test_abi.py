@@ -33,6 +33,28 @@ def test_library_exports_every_header_symbol():
     assert lib.noc_abi_version() == 5
 
 
+def test_stale_library_is_refused(tmp_path, monkeypatch):
+    """Build provenance: libnoc_hip.so carries the sha256 of the sources it was built from
+    (noc_build_hash, baked in by the Makefile) and load() refuses it against a tree whose sources
+    differ by one byte -- a stale binary cannot pass for the current sources."""
+    import shutil
+    from noc import _lib
+    monkeypatch.delenv("NOC_ALLOW_STALE_LIB", raising=False)
+    lib = _lib.load()
+    assert lib.noc_build_hash().decode() == _lib.tree_build_hash()
+    pkg = os.path.join(ROOT, "ip-parallel-optimal-control_amd")
+    copy = tmp_path / "pkg"
+    shutil.copytree(os.path.join(pkg, "csrc"), copy / "csrc")
+    os.makedirs(tmp_path / "include")
+    shutil.copy(HEADER, tmp_path / "include")
+    assert _lib.tree_build_hash(str(copy)) == _lib.tree_build_hash()
+    _lib.load(_lib.LIB_PATH, pkg_root=str(copy))  # the same sources: accepted
+    f = copy / "csrc" / "small_linalg.h"
+    f.write_bytes(f.read_bytes() + b" ")
+    with pytest.raises(_lib.NocError, match="built from other sources"):
+        _lib.load(_lib.LIB_PATH, pkg_root=str(copy))
+
+
 def test_supported_shapes_and_lanes():
     from noc import _lib
     lib = _lib.load()

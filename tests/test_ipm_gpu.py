@@ -228,6 +228,78 @@ def test_persistent_states_in_lds_equal_workspace(name, mode, monkeypatch):
     assert np.array_equal(Ul, Uw) and np.array_equal(Xl, Xw)
 
 
+def _struct_problem(name, N, Bt):
+    """(ocp, x0, u0) of a built-in family (c2 / c3 shapes) or a registered one (parametrised cost:
+    the actuated pendulum, nx = 3; traced cost: the track-limited cart-pole)."""
+    from noc import problems
+    if name in ("pendulum", "cartpole"):
+        return (problems.make_problem(name, N),) + tuple(problems.initial_conditions(name, N, Bt, seed=31))
+    import custom_families as CF
+    if name == "actuated_pendulum":
+        rng = np.random.default_rng(7)
+        x0 = np.array([0.1, -0.1, 0.0]) + 0.01 * rng.normal(size=(Bt, 3))
+        return CF.actuated_pendulum(1.0 / N), x0, 0.1 * rng.normal(size=(Bt, N, 1))
+    return (CF.cartpole_track_limit(1.0 / N),) + tuple(problems.initial_conditions("cartpole", N, Bt, seed=3))
+
+
+@pytest.mark.parametrize("name,N,Bt,mode", [
+    ("pendulum", 100, 1024, "par"),        # c2
+    ("cartpole", 200, 4096, "par"),        # c3: probe launch capped at 32 solves + resume
+    ("cartpole", 60, 96, "seq"),
+    ("actuated_pendulum", 50, 64, "par"),  # registered, parametrised cost, nx = 3
+    ("cartpole_track_limit", 60, 64, "par"),  # registered, traced cost with a state constraint
+])
+def test_structured_blocks_equal_dense_instance(name, N, Bt, mode, monkeypatch):
+    """The persistent solver's structure-aware blocks (csrc/block_struct.h: only the variable
+    entries of A, B, Q, R, M in the workspace, the constant ones rebuilt from literals and the
+    family's parameters, products with structural zeros skipped) against the dense instance
+    (NOC_PERSIST_STRUCT=0): bit-identical controls and states, identical counters."""
+    monkeypatch.setenv("NOC_PERSIST_WIDE", "0")
+    from noc import _lib
+    from noc.ipm import BatchedIPM
+    ocp, x0, u0 = _struct_problem(name, N, Bt)
+    m = _lib.MODE_PAR if mode == "par" else _lib.MODE_SEQ
+    res = []
+    for struct in ("1", "0"):
+        monkeypatch.setenv("NOC_PERSIST_STRUCT", struct)
+        eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
+        eng.load(u0, x0)
+        eng.solve(mode=m)
+        torch.cuda.synchronize()
+        res.append([t.cpu().numpy() for t in eng.result()] + [eng.t["x"].cpu().numpy(),
+                                                             eng.t["phase"].cpu().numpy()])
+    (Us, its, ss, Xs, phs), (Ud, itd, sd, Xd, phd) = res
+    assert np.all(phs == _lib.PHASE_DONE) and np.all(phd == _lib.PHASE_DONE)
+    assert np.array_equal(its, itd) and np.array_equal(ss, sd)
+    assert np.array_equal(Us, Ud) and np.array_equal(Xs, Xd)
+
+
+def test_structured_resume_after_launch_per_phase_driver(monkeypatch):
+    """A SOLVE resume of the persistent solver recomputes the blocks instead of reading the
+    workspace's: after the launch-per-phase driver (dense blocks in the workspace) it continues
+    exactly like a persistent solve capped at the same point (compact blocks)."""
+    monkeypatch.setenv("NOC_PERSIST_WIDE", "0")
+    from noc import problems, _lib
+    from noc.ipm import BatchedIPM
+    N, Bt = 80, 32
+    ocp = problems.make_problem("cartpole", N)
+    x0, u0 = problems.initial_conditions("cartpole", N, Bt, seed=12)
+    ref = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
+    ref.load(u0, x0)
+    ref.solve_persistent(schedule="index")
+    eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=False)
+    eng.load(u0, x0)
+    eng.init(0.1)
+    for _ in range(3):  # a few device iterations leave trajectories mid-retry (phase SOLVE) too
+        eng.step(_lib.MODE_PAR, _lib.TERMINAL_STAGE0)
+    eng.solve_persistent(resume=True)
+    torch.cuda.synchronize()
+    a, b = ref.result(), eng.result()
+    assert np.array_equal(a[1].cpu().numpy(), b[1].cpu().numpy())
+    assert np.array_equal(a[2].cpu().numpy(), b[2].cpu().numpy())
+    assert _rel(b[0].cpu().numpy(), a[0].cpu().numpy()) < 1e-12
+
+
 @pytest.mark.parametrize("wide", ["0", "1"])
 def test_persistent_solve_respects_solve_cap(wide, monkeypatch):
     """A trajectory that reaches max_solves stops (phase != DONE) -- every wave exits (the one-wave
