@@ -9,7 +9,12 @@ from noc import problems, _lib
 from noc.ipm import BatchedIPM
 lib = _lib.load()
 names = ["rollout", "linearize", "costate_blocks", "kkt", "trial", "iterations"]
-for name, N, B in [("pendulum", 50, 1), ("cartpole", 200, 1), ("cartpole", 200, 4096)]:
+# one-wave kernel throughout (B = 1 would run the wide kernel); both block layouts (round 6:
+# NOC_PERSIST_STRUCT=1 structure-aware compact blocks, 0 dense)
+os.environ["NOC_PERSIST_WIDE"] = "0"
+CONFIGS = [("pendulum", 50, 1), ("cartpole", 200, 1), ("cartpole", 200, 512), ("cartpole", 200, 4096)]
+for name, N, B, struct in [c + (s,) for c in CONFIGS for s in ("1", "0")]:
+    os.environ["NOC_PERSIST_STRUCT"] = struct
     ocp = problems.make_problem(name, N)
     x0, u0 = problems.initial_conditions(name, N, B, seed=11)
     eng = BatchedIPM(ocp.family, N, B, persistent=True)
@@ -22,5 +27,5 @@ for name, N, B in [("pendulum", 50, 1), ("cartpole", 200, 1), ("cartpole", 200, 
     lib.noc_debug_phase_cycles(buf, 8, 1)
     c = {k: int(buf[i]) for i, k in enumerate(names)}
     its = max(c["iterations"], 1)
-    print(json.dumps({"problem": name, "N": N, "B": B, "ms": e0.elapsed_time(e1),
+    print(json.dumps({"problem": name, "N": N, "B": B, "struct": struct, "ms": e0.elapsed_time(e1),
                       "cycles_per_iteration": {k: c[k] / its for k in names[:5]}, "totals": c}), flush=True)
