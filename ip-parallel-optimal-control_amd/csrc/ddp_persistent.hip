@@ -301,7 +301,7 @@ __global__ __launch_bounds__(64) void ddp_solve_kernel(noc_family prm, DdpArgs a
         const double gain = (new_cost - cost) / pred;               // D:126-127
         success = (gain > 0.0) && feas;                             // D:128
         const double rp_used = rp;
-        rp = success ? rp * fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0))
+        rp = success ? rp * rp_shrink(gain)
                      : rp * reg_inc;                                // D:129-133: the OUTER reg_inc
         r_inc = success ? 2.0 : 2.0 * r_inc;                        // D:133
         rp = fmin(fmax(rp, 1e-16), 1e16);                           // D:135

@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256) void trial_kernel(noc_family prm, noc_ipm_ws w
   const bool success = (gain > 0.0) && bwd_ok;            // P:166 / S:137
   double rp = w.rp[b], rinc = w.rinc[b];
   const double rp_used = rp;
-  const double shrink = fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0));
+  const double shrink = rp_shrink(gain);  // P:169 / S:141 (noc_internal.h)
   rp = success ? rp * shrink : rp * rinc;                 // P:167-171 / S:139-143
   rinc = success ? 2.0 : 2.0 * rinc;                      // P:172 / S:144
   bool take, end_iter, stop;

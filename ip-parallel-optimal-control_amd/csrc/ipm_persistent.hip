@@ -132,11 +132,14 @@ struct CompactSrc {
 template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS, bool STRUCT>
 __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
                                                          int terminal, double bp0,
-                                                         int max_solves) {
+                                                         int max_solves, int prio_n) {
   // one wave (= one 64-thread workgroup) per trajectory; w.order: the launch order (a permutation)
   const int b = w.order ? w.order[blockIdx.x] : (int)blockIdx.x;
   const int l = threadIdx.x;
   if (b < 0 || b >= w.Bt) return;  // an out-of-range order entry solves nothing (never faults)
+  // the first prio_n workgroups of an ordered launch (the costliest trajectories first) issue
+  // ahead of the waves they share a SIMD with (NOC_PERSIST_PRIO; 0 = off)
+  if (w.order && (int)blockIdx.x < prio_n) __builtin_amdgcn_s_setprio(2);
   constexpr int KD = kd_width<NX, NU>();
   Fam<KIND, NX, NU> f(prm);
   using BS = BlockStruct<KIND, NX, NU, STRUCT>;
@@ -533,7 +536,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       if (l == 0) NOC_TRACE_DECISION(g_dtrace, b, solves, bp, it, inner, cost, new_cost, pred, gain,
                                      success, rp, rinc, hu, bwd_ok);
 #endif
-      const double shrink = fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0));
+      const double shrink = rp_shrink(gain);  // P:169 / S:141 (noc_internal.h)
       const double rp_used = rp;
       rp = success ? rp * shrink : rp * rinc;                   // P:167-171 / S:139-143
       rinc = success ? 2.0 : 2.0 * rinc;                        // P:172 / S:144
@@ -648,12 +651,14 @@ static hipError_t launch_solve(const noc_family& p, const noc_ipm_ws& w, int mod
                                double bp0, int max_solves, size_t lds, hipStream_t s) {
   // the structure-aware blocks unless NOC_PERSIST_STRUCT=0 (per launch: tests switch it)
   const char* senv = getenv("NOC_PERSIST_STRUCT");
+  const char* penv = getenv("NOC_PERSIST_PRIO");  // experiment: raised priority for the first K
+  const int prio_n = penv ? atoi(penv) : 0;
   if (senv && atoi(senv) == 0)
     hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, WPS, RESUME, XLDS, false>), dim3(w.Bt), dim3(64),
-                       lds, s, p, w, mode, terminal, bp0, max_solves);
+                       lds, s, p, w, mode, terminal, bp0, max_solves, prio_n);
   else
     hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, WPS, RESUME, XLDS, true>), dim3(w.Bt), dim3(64),
-                       lds, s, p, w, mode, terminal, bp0, max_solves);
+                       lds, s, p, w, mode, terminal, bp0, max_solves, prio_n);
   return hipGetLastError();
 }
 

@@ -649,7 +649,7 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
       if (t == 0) NOC_TRACE_DECISION(g_wide_dtrace, b, solves, bp, it, inner, cost, new_cost, pred,
                                      gain, success, rp, rinc, hu, bwd_ok);
 #endif
-      const double shrink = fmax(1.0 / 3.0, 1.0 - (2.0 * gain - 1.0) * (2.0 * gain - 1.0) * (2.0 * gain - 1.0));
+      const double shrink = rp_shrink(gain);  // P:169 / S:141 (noc_internal.h)
       const double rp_used = rp;
       rp = success ? rp * shrink : rp * rinc;                   // P:167-171 / S:139-143
       rinc = success ? 2.0 : 2.0 * rinc;                        // P:172 / S:144

@@ -16,6 +16,13 @@
 #define NOC_KKT_SHAPES_DEF "kkt_shapes.def"
 #endif
 
+// gfx950 (MI355X) only: the launchers size LDS budgets for its 160 KB per CU (the 40 KB per wave
+// of the one-wave-per-SIMD instances, kkt_scan_impl.h: AB) and the cache policy for its 256 MiB
+// memory-side cache (kkt_nt3); on another target those sizes would be wrong, so refuse to build.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "libnoc_hip targets gfx950 (MI355X) only: LDS budgets and cache policies are sized for it"
+#endif
+
 namespace noc {
 
 enum KKTMode : int { MODE_FULL = 0, MODE_BWD = 1, MODE_FWD = 2 };
@@ -120,6 +127,17 @@ inline size_t kkt_lds_bytes_rt(int nx, int nu, int N, int L) {
   const size_t segs = L >= 64 ? 1 : 64 / L;  // trajectories per workgroup (L = 128: two waves)
   const size_t bytes = segs * per_traj * sizeof(double);
   return bytes <= 20480 * (size_t)(L > 64 ? L / 64 : 1) ? bytes : 0;
+}
+
+// The regularisation shrink factor max(1/3, 1 - (2 gain - 1)^3) of P:169 / S:141 / D:131 with
+// JAX's rounding: `x ** 3` with an int exponent is lax.integer_pow, x * (x * x), and 1 - that
+// rounds once more -- so no FMA contraction here (it would fuse the last multiply with the
+// subtraction: one rounding instead of two, a last-bit difference in rp that steers every later
+// step).  oracle/noc_oracle.py: _cube; tests/test_ipm_gpu.py checks every accepted step's rp.
+__device__ __forceinline__ double rp_shrink(double gain) {
+#pragma clang fp contract(off)
+  const double c = 2.0 * gain - 1.0;
+  return fmax(1.0 / 3.0, 1.0 - c * (c * c));
 }
 
 // Retry fixed point of the par inner loop (P:151-188).  A rejected trial whose rp was already at

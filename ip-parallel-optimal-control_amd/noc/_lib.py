@@ -19,8 +19,9 @@ _COMMON_SOURCES = ("csrc/small_linalg.h", "csrc/noc_internal.h", "csrc/kkt_shape
                    "../include/noc_hip.h")
 KKT_KERNEL_SOURCES = {
     "kkt_scan": ("csrc/kkt_scan_impl.h", "csrc/kkt_scan_2x1.hip", "csrc/kkt_scan_4x1.hip",
-                 "csrc/kkt_scan_8x4.hip", "csrc/kkt_scan_8x4_l32.hip", "csrc/kkt_scan_8x4_l16.hip",
-                 "csrc/kkt_scan_8x4_l8.hip") + _COMMON_SOURCES,
+                 "csrc/kkt_scan_4x1_l32.hip", "csrc/kkt_scan_4x1_l32nt.hip",
+                 "csrc/kkt_scan_4x1_l128.hip", "csrc/kkt_scan_8x4.hip", "csrc/kkt_scan_8x4_l32.hip",
+                 "csrc/kkt_scan_8x4_l16.hip", "csrc/kkt_scan_8x4_l8.hip") + _COMMON_SOURCES,
     "kkt_group8": ("csrc/kkt_group_impl.h", "csrc/kkt_group8_impl.h", "csrc/kkt_group.hip")
     + _COMMON_SOURCES,
 }

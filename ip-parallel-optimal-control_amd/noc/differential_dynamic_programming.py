@@ -210,8 +210,8 @@ def _solve_blocks(ocp, U, X0, bp0, max_passes, flags):
                                        total_cost(ocp, xt, ut, bp), inf)  # D:121-125
                 gain = (new_cost - cost) / pred
                 succ = (gain > 0) & feas
-                rp_new = torch.where(succ, rp * torch.clamp(1.0 - (2.0 * gain - 1.0) ** 3,
-                                                            min=1.0 / 3.0),
+                c = 2.0 * gain - 1.0  # x ** 3 as lax.integer_pow: c * (c * c), then 1 - it
+                rp_new = torch.where(succ, rp * torch.clamp(1.0 - c * (c * c), min=1.0 / 3.0),
                                      rp * reg_inc)  # D:129-133: the outer reg_inc
                 r_inc_new = torch.where(succ, torch.full_like(r_inc, 2.0), 2.0 * r_inc)
                 rp = torch.where(retry, rp_new.clamp(1e-16, 1e16), rp)

@@ -70,12 +70,22 @@ def compute_derivatives(ocp: OCP, states, controls, bp) -> Derivatives:
     dynamics at (x_k, u_k), k < N (noc_derivatives).  states (N+1, nx), controls (N, nu) (or
     batched), bp a scalar or one per trajectory."""
     fam = _family(ocp)
+    nx, nu = fam.nx, fam.nu
+    # every size from the states, the controls checked against them on the host, before anything
+    # reaches the device
+    xs = _shape(states)
+    single = len(xs) == 2
+    B = 1 if single else (xs[0] if len(xs) == 3 else -1)
+    N = xs[-2] - 1 if len(xs) in (2, 3) else -1
+    _expect_shapes("compute_derivatives", single, B,
+                   [("states", states, (N + 1, nx)), ("controls", controls, (N, nu))])
     x, u = _dev(states, "states"), _dev(controls, "controls")
-    single = x.dim() == 2
     if single:
         x, u = x[None], u[None]
-    B, N, nx, nu = u.shape[0], u.shape[1], fam.nx, fam.nu
-    bpt = torch.as_tensor(bp, dtype=torch.float64, device=x.device).reshape(-1).expand(B).contiguous()
+    bpt = torch.as_tensor(bp, dtype=torch.float64, device=x.device).reshape(-1)
+    if bpt.numel() not in (1, B):
+        raise _lib.NocError(f"compute_derivatives: bp needs 1 or {B} values, got {bpt.numel()}")
+    bpt = bpt.expand(B).contiguous()
     f64 = dict(dtype=torch.float64, device=x.device)
     shapes = dict(cx=(nx,), cu=(nu,), cxx=(nx, nx), cuu=(nu, nu), cxu=(nx, nu), fx=(nx, nx),
                   fu=(nx, nu), fxx=(nx, nx, nx), fuu=(nx, nu, nu), fxu=(nx, nx, nu))
@@ -91,14 +101,24 @@ def compute_derivatives(ocp: OCP, states, controls, bp) -> Derivatives:
 def compute_lqr_params(lagrange_multipliers, d: Derivatives):
     """P:31-42: ru = cu + fu' l, Q = cxx + l.fxx, R = cuu + l.fuu, M = cxu + l.fxu with
     l = lambda[1:] (noc_lqr_params)."""
+    # sizes from lambda (N+1, nx) and cu (N, nu); lambda and every Derivatives field checked
+    # against them on the host, before anything reaches the device
+    ls, cus = _shape(lagrange_multipliers), _shape(d.cu)
+    single = len(ls) == 2
+    B = 1 if single else (ls[0] if len(ls) == 3 else -1)
+    N = ls[-2] - 1 if len(ls) in (2, 3) else -1
+    nx = ls[-1] if len(ls) in (2, 3) else -1
+    nu = cus[-1] if len(cus) >= 1 else -1
+    shapes = dict(cx=(nx,), cu=(nu,), cxx=(nx, nx), cuu=(nu, nu), cxu=(nx, nu), fx=(nx, nx),
+                  fu=(nx, nu), fxx=(nx, nx, nx), fuu=(nx, nu, nu), fxu=(nx, nx, nu))
+    _expect_shapes("compute_lqr_params", single, B,
+                   [("lagrange_multipliers", lagrange_multipliers, (N + 1, nx))] +
+                   [(k, getattr(d, k), (N,) + shapes[k]) for k in Derivatives._fields])
     lam = _dev(lagrange_multipliers, "lagrange_multipliers")
     dd = Derivatives(*(_dev(t) for t in d))
-    single = lam.dim() == 2
     if single:
         lam = lam[None]
         dd = Derivatives(*(t[None] for t in dd))
-    B, N, nu = dd.cu.shape
-    nx = lam.shape[-1]
     f64 = dict(dtype=torch.float64, device=lam.device)
     ru, Q, R, M = (torch.empty(B, N, *s, **f64) for s in ((nu,), (nx, nx), (nu, nu), (nx, nu)))
     lib = _lib.load()

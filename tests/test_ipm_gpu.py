@@ -429,6 +429,29 @@ def test_wide_solve_matches_one_wave_kernel(name, N, Bt, mode, monkeypatch):
         assert np.max(np.abs(Uw[b] - Un[b])) <= 1e-6 * max(1.0, float(np.max(np.abs(Un))))
 
 
+def test_rp_update_rounds_like_the_reference():
+    """The regularisation update after an accepted step, rp * max(1/3, 1 - (2 gain - 1) ** 3)
+    (P:167-173, S:139-143), rounds like the reference: the cube as lax.integer_pow, c * (c * c),
+    then the subtraction -- no fused multiply-subtract (noc_internal.h: rp_shrink; the oracle's
+    _cube).  Checked bit for bit on every accepted step of par and seq solves of both persistent
+    kernels from the decision-trace build (tools/rp_trace_check.py), which must also contain
+    gains where a fused evaluation would have rounded differently."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    tlib = os.path.join(root, "ip-parallel-optimal-control_amd", "noc", "_lib", "libnoc_hip_trace.so")
+    assert os.path.exists(tlib), "decision-trace build missing (make trace-lib / build())"
+    env = dict(os.environ, NOC_HIP_LIB=tlib)
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "rp_trace_check.py")],
+                       check=True, env=env, capture_output=True, text=True, timeout=240)
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    for k, v in res.items():
+        assert v["checked"] > 20 and v["mismatched"] == 0, (k, v)
+    assert sum(v["fused_would_differ"] for v in res.values()) > 0, res
+
+
 def _resume_case(name, N, Bt, seed=5):
     from noc import problems
     ocp = problems.make_problem(name, N)

@@ -73,6 +73,32 @@ def test_ddp_bwd_pass_rejects_mis_shaped_final_state_and_reg():
         ddp_mod.bwd_pass(ocp, np.zeros((B, 4)), _derivs(4, 1, batch=B), np.ones(B + 1))
 
 
+@pytest.mark.parametrize("xs,us", [
+    ((N + 1, 4), (B, N, 1)),     # unbatched states, batched controls (N would read as B)
+    ((B, N + 1, 4), (N, 1)),     # batched states, unbatched controls
+    ((B, N, 4), (B, N, 1)),      # states without the terminal row
+    ((B, N + 1, 3), (B, N, 1)),  # wrong state dimension
+    ((B, N + 1, 4), (B + 1, N, 1)),  # batch sizes disagree
+])
+def test_compute_derivatives_rejects_mis_shaped_inputs(xs, us):
+    with pytest.raises(_lib.NocError, match="compute_derivatives"):
+        par.compute_derivatives(_cartpole(), np.zeros(xs), np.zeros(us), 0.1)
+
+
+@pytest.mark.parametrize("field", list(Derivatives._fields))
+def test_compute_lqr_params_rejects_any_mis_shaped_derivative(field):
+    d = _derivs(4, 1, batch=B)
+    bad = np.zeros(getattr(d, field).shape[:-1] + (getattr(d, field).shape[-1] + 1,))
+    with pytest.raises(_lib.NocError, match="compute_lqr_params"):
+        par.compute_lqr_params(np.zeros((B, N + 1, 4)), d._replace(**{field: bad}))
+
+
+def test_compute_lqr_params_rejects_mis_shaped_lambda():
+    for lam in (np.zeros((B, N, 4)), np.zeros((N + 1, 4)), np.zeros((B + 1, N + 1, 4))):
+        with pytest.raises(_lib.NocError, match="compute_lqr_params"):
+            par.compute_lqr_params(lam, _derivs(4, 1, batch=B))
+
+
 def test_well_shaped_inputs_pass_the_host_checks():
     """Correct shapes get past the checks: the next thing that happens is the device transfer,
     which on a CPU-only host raises for the missing GPU, never a shape error."""
@@ -82,6 +108,8 @@ def test_well_shaped_inputs_pass_the_host_checks():
         lambda: par.nonlin_rollout(ocp, np.zeros((N, 1, 4)), np.zeros((N, 1)), np.zeros((N + 1, 4)),
                                    np.zeros((N, 1))),
         lambda: ddp_mod.bwd_pass(ocp, np.zeros(4), _derivs(4, 1), 1e-3),
+        lambda: par.compute_derivatives(ocp, np.zeros((B, N + 1, 4)), np.zeros((B, N, 1)), 0.1),
+        lambda: par.compute_lqr_params(np.zeros((N + 1, 4)), _derivs(4, 1)),
     ]
     for call in calls:
         try:
