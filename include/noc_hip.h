@@ -173,7 +173,9 @@ typedef struct noc_ipm_ws {
   int lanes;                           /* tiled layout of A,B,Q,R,M,r,K,d (8/16/32/64)  */
   int flags;                           /* NOC_WS_* bits (0 = the whole barrier schedule) */
   double *x, *u, *x0;                  /* (Bt,N+1,nx) (Bt,N,nu) (Bt,nx)           */
-  double *A, *B, *Q, *R, *M, *r, *P;   /* LQ blocks: tiled (P natural)              */
+  double *A, *B, *Q, *R, *M, *r, *P;   /* LQ blocks: tiled (P natural).  noc_ipm_solve
+                                          keeps only their variable entries here (compact
+                                          records, csrc/block_struct.h): scratch after it */
   double *cx, *cu, *lc, *lam;          /* cx, cu, lc tiled (E = nx, nu, 1); lam (Bt,N+1,nx).
                                           cx, cu, lam: written by the launch-per-phase driver
                                           only (noc_ipm_solve keeps them in registers) */

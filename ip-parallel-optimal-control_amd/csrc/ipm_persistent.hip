@@ -767,8 +767,11 @@ static bool use_wide(const noc_family& p, const noc_ipm_ws& w) {
 
 hipError_t ipm_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal, double bp0,
                      int max_solves, hipStream_t s) {
-  if (use_wide(p, w))
-    return ipm_solve_wide(p, w, mode, terminal, bp0, max_solves, nullptr, nullptr, w.Bt, s);
+  if (use_wide(p, w)) {
+    static const int cus = device_simds() / 4;
+    return ipm_solve_wide(p, w, mode, terminal, bp0, max_solves, nullptr, nullptr, w.Bt,
+                          wide_waves(p, w, cus), s);
+  }
 #define NOC_FAMILY(K, X, U)                                                              \
   if (p.kind == K && p.nx == X && p.nu == U)                                             \
     return solve_family<K, X, U>(p, w, mode, terminal, bp0, max_solves, s);

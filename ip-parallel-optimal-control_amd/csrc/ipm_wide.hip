@@ -22,6 +22,7 @@
 #include <cstdlib>
 
 #include "../../include/noc_hip.h"
+#include "block_struct.h"
 #include "ipm_family.h"
 #include "kkt_scan_impl.h"
 #include "noc_internal.h"
@@ -47,21 +48,23 @@ namespace {
 
 constexpr int kWideWaves = 4;
 
-// LDS image of one trajectory (offsets in doubles)
-template <int NX, int NU>
+// LDS image of one trajectory (offsets in doubles).  A, B, Q, R, M hold only the variable entries
+// of the blocks (BS = BlockStruct: block_struct.h; the constants are rebuilt where they are read),
+// which cuts cart-pole N = 200 from 84.5 to 47 KB -- two workgroups per CU for the two-wave
+// instance.
+template <int NX, int NU, class BS>
 struct WideLds {
   static constexpr int KD = NU * (NX + 1);
-  static constexpr int SQ = Sym<NX>::SZ, SR = Sym<NU>::SZ;
   int x, u, A, B, Q, R, M, r, cx, cu, lc, kd, agg, red, P, total;
   __host__ __device__ WideLds(int N, int W) {
     int o = 0;
     x = o; o += (N + 1) * NX;
     u = o; o += N * NU;
-    A = o; o += NX * NX * N;
-    B = o; o += NX * NU * N;
-    Q = o; o += SQ * N;
-    R = o; o += SR * N;
-    M = o; o += NX * NU * N;
+    A = o; o += BS::template nv<BF_A>() * N;
+    B = o; o += BS::template nv<BF_B>() * N;
+    Q = o; o += BS::template nv<BF_Q>() * N;
+    R = o; o += BS::template nv<BF_R>() * N;
+    M = o; o += BS::template nv<BF_M>() * N;
     r = o; o += NU * N;
     cx = o; o += NX * N;
     cu = o; o += NU * N;
@@ -81,6 +84,21 @@ NOC_DEV void fget(const double* base, int N, int s, double* v) {
 template <int E>
 NOC_DEV void fput(double* base, int N, int s, const double* v) {
   NOC_UNROLL for (int e = 0; e < E; ++e) base[(size_t)e * N + s] = v[e];
+}
+// a block field through its compact record: the variable entries stored, the constants rebuilt
+template <class BS, int F>
+NOC_DEV void bput(double* base, int N, int s, const double* full) {
+  constexpr int EV = BS::template nv<F>();
+  double v[EV > 0 ? EV : 1];
+  BS::template compress<F>(full, v);
+  fput<EV>(base, N, s, v);
+}
+template <class BS, int F>
+NOC_DEV void bget(const noc_family& p, const double* base, int N, int s, double* full) {
+  constexpr int EV = BS::template nv<F>();
+  double v[EV > 0 ? EV : 1];
+  fget<EV>(base, N, s, v);
+  BS::template expand<F>(p, v, full);
 }
 
 template <int NX>
@@ -113,6 +131,7 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
                                                              const int* count) {
   constexpr int T = 64 * W;
   constexpr int KD = NU * (NX + 1);
+  using BS = BlockStruct<KIND, NX, NU, true>;
   constexpr int ESZ = NX * NX + 2 * NX + 2 * Sym<NX>::SZ;  // scan element in doubles
   static_assert(ESZ <= 64 && NX * NX + NX <= 64, "aggregate slot");
   extern __shared__ __attribute__((aligned(16))) double noc_smem[];
@@ -127,7 +146,7 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
   const int b = idx ? idx[jb] : jb;
   Fam<KIND, NX, NU> f(prm);
   const int N = w.N;
-  const WideLds<NX, NU> L(N, W);
+  const WideLds<NX, NU, BS> L(N, W);
   double* sx = noc_smem + L.x;
   double* su = noc_smem + L.u;
   double* sA = noc_smem + L.A;
@@ -226,9 +245,11 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
           NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = sx[(size_t)s * NX + i];
           NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = su[(size_t)j * N + s];
           f.jac(x, u, fx, fu);
+          BS::template fold_consts<BF_A>(prm, fx);
+          BS::template fold_consts<BF_B>(prm, fu);
           f.stage_grad(x, u, bp, cx, cu);
-          fput<NX * NX>(sA, N, s, fx);
-          fput<NX * NU>(sB, N, s, fu);
+          bput<BS, BF_A>(sA, N, s, fx);
+          bput<BS, BF_B>(sB, N, s, fu);
           fput<NX>(scx, N, s, cx);
           fput<NU>(scu, N, s, cu);
           slc[s] = f.stage_cost(x, u, bp);
@@ -245,17 +266,17 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
         set_zero(g);
         for (int s = start + len - 1; s >= start; --s) {
           double A[NX * NX], cx[NX];
-          fget<NX * NX>(sA, N, s, A);
+          bget<BS, BF_A>(prm, sA, N, s, A);
           fget<NX>(scx, N, s, cx);
           Mat<NX, NX> Gn;
           Vec<NX> gn;
           NOC_UNROLL for (int i = 0; i < NX; ++i) {
             double a = cx[i];
-            NOC_UNROLL for (int m = 0; m < NX; ++m) a += A[m * NX + i] * g[m];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) if (BS::nzA(m, i)) a += A[m * NX + i] * g[m];
             gn[i] = a;
             NOC_UNROLL for (int j = 0; j < NX; ++j) {
               double c = 0.0;
-              NOC_UNROLL for (int m = 0; m < NX; ++m) c += A[m * NX + i] * G(m, j);
+              NOC_UNROLL for (int m = 0; m < NX; ++m) if (BS::nzA(m, i)) c += A[m * NX + i] * G(m, j);
               Gn(i, j) = c;
             }
           }
@@ -328,37 +349,40 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
           double x[NX], u[NU], A[NX * NX], Bm[NX * NU], cx[NX], cu[NU];
           NOC_UNROLL for (int i = 0; i < NX; ++i) x[i] = sx[(size_t)s * NX + i];
           NOC_UNROLL for (int j = 0; j < NU; ++j) u[j] = su[(size_t)j * N + s];
-          fget<NX * NX>(sA, N, s, A);
-          fget<NX * NU>(sB, N, s, Bm);
+          bget<BS, BF_A>(prm, sA, N, s, A);
+          bget<BS, BF_B>(prm, sB, N, s, Bm);
           fget<NX>(scx, N, s, cx);
           fget<NU>(scu, N, s, cu);
           // Q = cxx + l.fxx, R = cuu + l.fuu, M = cxu + l.fxu at l = lambda_{s+1} (P:35-37)
           double Qf[NX * NX], Rf[NU * NU], M[NX * NU], rr[NU];
           f.stage_hess(x, u, bp, Qf, Rf, M);
           f.add_hess_l(x, u, lam, Qf, Rf, M);
+          BS::template fold_consts<BF_M>(prm, M);
           Sym<NX> Qs;
           Sym<NU> Rs;
           NOC_UNROLL for (int i = 0; i < NX; ++i)
             NOC_UNROLL for (int j = i; j < NX; ++j) Qs(i, j) = (i == j) ? Qf[i * NX + i] : 0.5 * (Qf[i * NX + j] + Qf[j * NX + i]);
           NOC_UNROLL for (int i = 0; i < NU; ++i)
             NOC_UNROLL for (int j = i; j < NU; ++j) Rs(i, j) = (i == j) ? Rf[i * NU + i] : 0.5 * (Rf[i * NU + j] + Rf[j * NU + i]);
+          BS::template fold_consts<BF_Q>(prm, Qs.v);
+          BS::template fold_consts<BF_R>(prm, Rs.v);
           NOC_UNROLL for (int j = 0; j < NU; ++j) {  // ru = cu + fu' lambda_{s+1} (P:34)
             double a = cu[j];
-            NOC_UNROLL for (int i = 0; i < NX; ++i) a += Bm[i * NU + j] * lam[i];
+            NOC_UNROLL for (int i = 0; i < NX; ++i) if (BS::nzB(i, j)) a += Bm[i * NU + j] * lam[i];
             rr[j] = a;
             red[1] = nan_max(red[1], fabs(a));
             red[2] += cu[j] * cu[j];
           }
-          fput<Sym<NX>::SZ>(sQ, N, s, Qs.v);
-          fput<Sym<NU>::SZ>(sR, N, s, Rs.v);
-          fput<NX * NU>(sM, N, s, M);
+          bput<BS, BF_Q>(sQ, N, s, Qs.v);
+          bput<BS, BF_R>(sR, N, s, Rs.v);
+          bput<BS, BF_M>(sM, N, s, M);
           fput<NU>(sr, N, s, rr);
           if (terminal == NOC_TERMINAL_STAGE0 && s == 0)  // XT = Q[0] (P:73)
             NOC_UNROLL for (int i = 0; i < NX; ++i) NOC_UNROLL for (int j = 0; j < NX; ++j) sP[i * NX + j] = Qs(i, j);
           double ln[NX];  // lambda_s = cx_s + fx_s' lambda_{s+1}
           NOC_UNROLL for (int i = 0; i < NX; ++i) {
             double a = cx[i];
-            NOC_UNROLL for (int m = 0; m < NX; ++m) a += A[m * NX + i] * lam[m];
+            NOC_UNROLL for (int m = 0; m < NX; ++m) if (BS::nzA(m, i)) a += A[m * NX + i] * lam[m];
             ln[i] = a;
           }
           NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = ln[i];
@@ -384,11 +408,11 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
       // ---------------- KKT solve (par_Newton, P:107-124) ----------------
       // phase 1: this lane's chunk element (Riccati-form prepend, kkt_scan_impl.h)
       auto stage_from_lds = [&](int s, StageData<NX, NU>& st) {
-        fget<NX * NX>(sA, N, s, st.A.v);
-        fget<NX * NU>(sB, N, s, st.B.v);
-        fget<Sym<NX>::SZ>(sQ, N, s, st.Q.v);
-        fget<Sym<NU>::SZ>(sR, N, s, st.R.v);
-        fget<NX * NU>(sM, N, s, st.M.v);
+        bget<BS, BF_A>(prm, sA, N, s, st.A.v);
+        bget<BS, BF_B>(prm, sB, N, s, st.B.v);
+        bget<BS, BF_Q>(prm, sQ, N, s, st.Q.v);
+        bget<BS, BF_R>(prm, sR, N, s, st.R.v);
+        bget<BS, BF_M>(prm, sM, N, s, st.M.v);
         fget<NU>(sr, N, s, st.r.v);
       };
       Sym<NX> Pt;
@@ -401,7 +425,7 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
       for (int s = start + len - 1; s >= start; --s) {
         StageData<NX, NU> st;
         stage_from_lds(s, st);
-        prepend<NX, NU, false>(e, st, reg);
+        prepend<NX, NU, false, BS>(e, st, reg);
       }
       NOC_WSUB(0);
       // phase 2: in-wave reverse Sklansky scan (the last wave's elements end at the terminal
@@ -459,12 +483,12 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
         NOC_UNROLL for (int i = 0; i < NX; ++i) {
           NOC_UNROLL for (int j = 0; j < NX; ++j) {
             double a = 0.0;
-            NOC_UNROLL for (int k = 0; k < NX; ++k) a += S(i, k) * st.A(k, j);
+            NOC_UNROLL for (int k = 0; k < NX; ++k) if (BS::nzA(k, j)) a += S(i, k) * st.A(k, j);
             SA(i, j) = a;
           }
           NOC_UNROLL for (int j = 0; j < NU; ++j) {
             double a = 0.0;
-            NOC_UNROLL for (int k = 0; k < NX; ++k) a += S(i, k) * st.B(k, j);
+            NOC_UNROLL for (int k = 0; k < NX; ++k) if (BS::nzB(k, j)) a += S(i, k) * st.B(k, j);
             SB(i, j) = a;
           }
         }
@@ -472,7 +496,7 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
         NOC_UNROLL for (int i = 0; i < NU; ++i)
           NOC_UNROLL for (int j = i; j < NU; ++j) {
             double a = (i == j) ? st.R(i, j) + reg : st.R(i, j);
-            NOC_UNROLL for (int k = 0; k < NX; ++k) a += st.B(k, i) * SB(k, j);
+            NOC_UNROLL for (int k = 0; k < NX; ++k) if (BS::nzB(k, i)) a += st.B(k, i) * SB(k, j);
             Quu(i, j) = a;
           }
         double Y[NU][NX + 1];
@@ -481,12 +505,12 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
         NOC_UNROLL for (int i = 0; i < NU; ++i) {
           NOC_UNROLL for (int j = 0; j < NX; ++j) {
             double a = st.M(j, i);
-            NOC_UNROLL for (int k = 0; k < NX; ++k) a += SB(k, i) * st.A(k, j);
+            NOC_UNROLL for (int k = 0; k < NX; ++k) if (BS::nzA(k, j)) a += SB(k, i) * st.A(k, j);
             Qux(i, j) = a;
             Y[i][j] = a;
           }
           double a = st.r[i];
-          NOC_UNROLL for (int k = 0; k < NX; ++k) a += st.B(k, i) * v[k];
+          NOC_UNROLL for (int k = 0; k < NX; ++k) if (BS::nzB(k, i)) a += st.B(k, i) * v[k];
           Qu[i] = a;
           Y[i][NX] = a;
         }
@@ -507,14 +531,14 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
         NOC_UNROLL for (int i = 0; i < NX; ++i)
           NOC_UNROLL for (int j = i; j < NX; ++j) {
             double a = st.Q(i, j);
-            NOC_UNROLL for (int k = 0; k < NX; ++k) a += st.A(k, i) * SA(k, j);
+            NOC_UNROLL for (int k = 0; k < NX; ++k) if (BS::nzA(k, i)) a += st.A(k, i) * SA(k, j);
             NOC_UNROLL for (int q = 0; q < NU; ++q) a += Qux(q, i) * Kk[q * NX + j];
             Sn(i, j) = a;
           }
         Vec<NX> vn;
         NOC_UNROLL for (int i = 0; i < NX; ++i) {
           double a = 0.0;
-          NOC_UNROLL for (int k = 0; k < NX; ++k) a += st.A(k, i) * v[k];
+          NOC_UNROLL for (int k = 0; k < NX; ++k) if (BS::nzA(k, i)) a += st.A(k, i) * v[k];
           NOC_UNROLL for (int q = 0; q < NU; ++q) a += Qux(q, i) * Kk[NU * NX + q];
           vn[i] = a;
         }
@@ -526,11 +550,11 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
         NOC_UNROLL for (int i = 0; i < NX; ++i) {
           NOC_UNROLL for (int j = 0; j < NX; ++j) {
             double a = st.A(i, j);
-            NOC_UNROLL for (int q = 0; q < NU; ++q) a += st.B(i, q) * Kk[q * NX + j];
+            NOC_UNROLL for (int q = 0; q < NU; ++q) if (BS::nzB(i, q)) a += st.B(i, q) * Kk[q * NX + j];
             F(i, j) = a;
           }
           double a = 0.0;
-          NOC_UNROLL for (int q = 0; q < NU; ++q) a += st.B(i, q) * Kk[NU * NX + q];
+          NOC_UNROLL for (int q = 0; q < NU; ++q) if (BS::nzB(i, q)) a += st.B(i, q) * Kk[NU * NX + q];
           fv[i] = a;
         }
         Mat<NX, NX> Pn;
@@ -596,8 +620,8 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
       for (int s = start; s < start + len; ++s) {
         double Kk[KD], A[NX * NX], Bm[NX * NU];
         NOC_UNROLL for (int i = 0; i < KD; ++i) Kk[i] = kds(i, s);
-        fget<NX * NX>(sA, N, s, A);
-        fget<NX * NU>(sB, N, s, Bm);
+        bget<BS, BF_A>(prm, sA, N, s, A);
+        bget<BS, BF_B>(prm, sB, N, s, Bm);
         double u[NU];
         NOC_UNROLL for (int i = 0; i < NU; ++i) {
           double a = Kk[NU * NX + i];
@@ -607,8 +631,8 @@ __global__ __launch_bounds__(64 * W, 1) void ipm_wide_kernel(noc_family prm, noc
         double xn[NX];
         NOC_UNROLL for (int i = 0; i < NX; ++i) {
           double a = 0.0;
-          NOC_UNROLL for (int k = 0; k < NX; ++k) a += A[i * NX + k] * x[k];
-          NOC_UNROLL for (int j = 0; j < NU; ++j) a += Bm[i * NU + j] * u[j];
+          NOC_UNROLL for (int k = 0; k < NX; ++k) if (BS::nzA(i, k)) a += A[i * NX + k] * x[k];
+          NOC_UNROLL for (int j = 0; j < NU; ++j) if (BS::nzB(i, j)) a += Bm[i * NU + j] * u[j];
           xn[i] = a;
         }
         // the K/d region is [KD][N+1] and dx / du reuse rows 0..NX-1 / NX..NX+NU-1 of it: the
@@ -742,27 +766,44 @@ int debug_wide_cycles(long long* out, int n, int reset) {
   return 0;
 }
 
-// LDS bytes of one wide workgroup, 0 if the trajectory does not fit (one workgroup per CU)
-size_t wide_lds_bytes(int nx, int nu, int N) {
-  int total = 0;
+// LDS bytes of one W-wave workgroup of family p, 0 if the trajectory does not fit in a CU
+template <int K, int X, int U>
+static size_t wide_lds_t(int N, int W) {
+  const size_t bytes = (size_t)WideLds<X, U, BlockStruct<K, X, U, true>>(N, W).total * sizeof(double);
+  return bytes <= 160 * 1024 - 1024 ? bytes : 0;
+}
+size_t wide_lds_bytes(const noc_family& p, int N, int W) {
 #define NOC_FAMILY(K, X, U) \
-  if (nx == X && nu == U) total = WideLds<X, U>(N, kWideWaves).total;
+  if (p.kind == K && p.nx == X && p.nu == U) return wide_lds_t<K, X, U>(N, W);
 #include NOC_FAMILIES_DEF
 #undef NOC_FAMILY
-  if (total == 0) return 0;
-  const size_t bytes = (size_t)total * sizeof(double);
-  return bytes <= 160 * 1024 - 1024 ? bytes : 0;
+  return 0;
+}
+
+// Waves per trajectory: 4 when the batch leaves CUs idle (B <= #CUs: one workgroup per CU), 2
+// when two two-wave workgroups fit a CU (512 registers per lane: one wave per SIMD) -- B up to
+// 2 x #CUs, the 8-GPU slice of c3.  NOC_WIDE_WAVES=2|4 forces one (per launch).
+int wide_waves(const noc_family& p, const noc_ipm_ws& w, int cus) {
+  const char* env = getenv("NOC_WIDE_WAVES");
+  if (env && (atoi(env) == 2 || atoi(env) == 4)) return atoi(env);
+  if (cus > 0 && w.Bt <= cus) return 4;
+  const size_t two = wide_lds_bytes(p, w.N, 2);
+  return (two > 0 && two <= 80 * 1024 - 512) ? 2 : 4;
 }
 
 template <int K, int X, int U>
 static hipError_t wide_family(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                               double bp0, int max_solves, const int* idx, const int* count,
-                              int grid, hipStream_t s) {
+                              int grid, int W, hipStream_t s) {
   if constexpr (X <= 4) {
-    const size_t lds = wide_lds_bytes(X, U, w.N);
+    const size_t lds = wide_lds_t<K, X, U>(w.N, W);
     if (lds == 0 || grid <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((ipm_wide_kernel<K, X, U, kWideWaves>), dim3(grid), dim3(64 * kWideWaves),
-                       lds, s, p, w, mode, terminal, bp0, max_solves, idx, count);
+    if (W == 2)
+      hipLaunchKernelGGL((ipm_wide_kernel<K, X, U, 2>), dim3(grid), dim3(128), lds, s, p, w, mode,
+                         terminal, bp0, max_solves, idx, count);
+    else
+      hipLaunchKernelGGL((ipm_wide_kernel<K, X, U, kWideWaves>), dim3(grid), dim3(64 * kWideWaves),
+                         lds, s, p, w, mode, terminal, bp0, max_solves, idx, count);
     return hipGetLastError();
   } else {
     return hipErrorInvalidValue;
@@ -770,15 +811,15 @@ static hipError_t wide_family(const noc_family& p, const noc_ipm_ws& w, int mode
 }
 
 bool ipm_wide_supported(const noc_family& p, int N) {
-  return family_supported(p) && p.nx <= 4 && wide_lds_bytes(p.nx, p.nu, N) > 0;
+  return family_supported(p) && p.nx <= 4 && wide_lds_bytes(p, N, kWideWaves) > 0;
 }
 
 hipError_t ipm_solve_wide(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                           double bp0, int max_solves, const int* idx, const int* count, int grid,
-                          hipStream_t s) {
+                          int W, hipStream_t s) {
 #define NOC_FAMILY(K, X, U)                                                              \
   if (p.kind == K && p.nx == X && p.nu == U)                                             \
-    return wide_family<K, X, U>(p, w, mode, terminal, bp0, max_solves, idx, count, grid, s);
+    return wide_family<K, X, U>(p, w, mode, terminal, bp0, max_solves, idx, count, grid, W, s);
 #include NOC_FAMILIES_DEF
 #undef NOC_FAMILY
   return hipErrorInvalidValue;

@@ -243,12 +243,13 @@ hipError_t ipm_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int ter
                      int max_solves, hipStream_t s);
 // wide whole-solve kernel (ipm_wide.hip): one 4-wave workgroup per trajectory, LDS-resident
 bool ipm_wide_supported(const noc_family& p, int N);
-size_t wide_lds_bytes(int nx, int nu, int N);
+size_t wide_lds_bytes(const noc_family& p, int N, int W);
+int wide_waves(const noc_family& p, const noc_ipm_ws& w, int cus);
 int debug_wide_cycles(long long* out, int n, int reset);
 // grid workgroups solve trajectories idx[0 .. *count) (idx == NULL: 0 .. Bt-1, count ignored)
 hipError_t ipm_solve_wide(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
                           double bp0, int max_solves, const int* idx, const int* count, int grid,
-                          hipStream_t s);
+                          int W, hipStream_t s);
 hipError_t relayout(int direction, int E, int sym_n, int N, int Bt, int L, const double* src,
                     double* dst, hipStream_t s);
 bool family_supported(const noc_family& p);

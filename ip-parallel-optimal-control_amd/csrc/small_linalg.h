@@ -37,7 +37,7 @@ template <int N>
 struct Sym {
   static constexpr int SZ = N * (N + 1) / 2;
   double v[SZ];
-  static NOC_DEV constexpr int idx(int i, int j) {
+  static __host__ __device__ constexpr int idx(int i, int j) {
     return i <= j ? i * N - (i * (i - 1)) / 2 + (j - i) : j * N - (j * (j - 1)) / 2 + (i - j);
   }
   NOC_DEV double& operator()(int i, int j) { return v[idx(i, j)]; }
