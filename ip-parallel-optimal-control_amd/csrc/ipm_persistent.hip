@@ -132,14 +132,11 @@ struct CompactSrc {
 template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS, bool STRUCT>
 __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
                                                          int terminal, double bp0,
-                                                         int max_solves, int prio_n) {
+                                                         int max_solves) {
   // one wave (= one 64-thread workgroup) per trajectory; w.order: the launch order (a permutation)
   const int b = w.order ? w.order[blockIdx.x] : (int)blockIdx.x;
   const int l = threadIdx.x;
   if (b < 0 || b >= w.Bt) return;  // an out-of-range order entry solves nothing (never faults)
-  // the first prio_n workgroups of an ordered launch (the costliest trajectories first) issue
-  // ahead of the waves they share a SIMD with (NOC_PERSIST_PRIO; 0 = off)
-  if (w.order && (int)blockIdx.x < prio_n) __builtin_amdgcn_s_setprio(2);
   constexpr int KD = kd_width<NX, NU>();
   Fam<KIND, NX, NU> f(prm);
   using BS = BlockStruct<KIND, NX, NU, STRUCT>;
@@ -646,25 +643,25 @@ static int device_simds() {
 template <int KIND>
 constexpr bool one_wave_instance() { return KIND == NOC_FAMILY_CARTPOLE; }
 
+// grid: workgroups = the entries of w.order this launch solves (w.Bt without an order)
 template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS>
 static hipError_t launch_solve(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
-                               double bp0, int max_solves, size_t lds, hipStream_t s) {
+                               double bp0, int max_solves, size_t lds, hipStream_t s, int grid) {
   // the structure-aware blocks unless NOC_PERSIST_STRUCT=0 (per launch: tests switch it)
   const char* senv = getenv("NOC_PERSIST_STRUCT");
-  const char* penv = getenv("NOC_PERSIST_PRIO");  // experiment: raised priority for the first K
-  const int prio_n = penv ? atoi(penv) : 0;
   if (senv && atoi(senv) == 0)
-    hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, WPS, RESUME, XLDS, false>), dim3(w.Bt), dim3(64),
-                       lds, s, p, w, mode, terminal, bp0, max_solves, prio_n);
+    hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, WPS, RESUME, XLDS, false>), dim3(grid), dim3(64),
+                       lds, s, p, w, mode, terminal, bp0, max_solves);
   else
-    hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, WPS, RESUME, XLDS, true>), dim3(w.Bt), dim3(64),
-                       lds, s, p, w, mode, terminal, bp0, max_solves, prio_n);
+    hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, WPS, RESUME, XLDS, true>), dim3(grid), dim3(64),
+                       lds, s, p, w, mode, terminal, bp0, max_solves);
   return hipGetLastError();
 }
 
 template <int KIND, int NX, int NU, int WPS>
 static hipError_t solve_w(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
-                          double bp0, int max_solves, size_t lds, hipStream_t s) {
+                          double bp0, int max_solves, size_t lds, hipStream_t s, int grid = -1) {
+  if (grid < 0) grid = w.Bt;
   // x, u in LDS (XLDS) when that keeps the residency the register budget allows: 8 waves per CU
   // at 2 waves per SIMD (<= 20 KB per wave), 4 at one wave per SIMD (<= 40 KB); longer horizons
   // keep them in the workspace.  NOC_PERSIST_XLDS=0 forces the workspace (A/B).
@@ -673,10 +670,49 @@ static hipError_t solve_w(const noc_family& p, const noc_ipm_ws& w, int mode, in
   const bool xlds = !(xenv && atoi(xenv) == 0) && xl <= (WPS == 1 ? 40960u : 20480u);
   const bool res = (w.flags & NOC_WS_RESUME) != 0;
   if (xlds)
-    return res ? launch_solve<KIND, NX, NU, WPS, true, true>(p, w, mode, terminal, bp0, max_solves, xl, s)
-               : launch_solve<KIND, NX, NU, WPS, false, true>(p, w, mode, terminal, bp0, max_solves, xl, s);
-  return res ? launch_solve<KIND, NX, NU, WPS, true, false>(p, w, mode, terminal, bp0, max_solves, lds, s)
-             : launch_solve<KIND, NX, NU, WPS, false, false>(p, w, mode, terminal, bp0, max_solves, lds, s);
+    return res ? launch_solve<KIND, NX, NU, WPS, true, true>(p, w, mode, terminal, bp0, max_solves, xl, s, grid)
+               : launch_solve<KIND, NX, NU, WPS, false, true>(p, w, mode, terminal, bp0, max_solves, xl, s, grid);
+  return res ? launch_solve<KIND, NX, NU, WPS, true, false>(p, w, mode, terminal, bp0, max_solves, lds, s, grid)
+             : launch_solve<KIND, NX, NU, WPS, false, false>(p, w, mode, terminal, bp0, max_solves, lds, s, grid);
+}
+
+// Heavy-first split of an ordered launch larger than one wave per SIMD (cart-pole): the first
+// `heavy` entries of w.order -- the costliest trajectories (the probe-ordered resume,
+// BatchedIPM.solve_persistent) -- run on the one-wave instance, a SIMD of their own, concurrently
+// with the rest on the two-wave instance (second stream, event fork / join).  Every trajectory's
+// result is the same on either instance (tested).  NOC_PERSIST_HEAVY=<n> sets the count.
+static int heavy_count(const noc_ipm_ws& w, int simds) {
+  const char* env = getenv("NOC_PERSIST_HEAVY");  // per launch (A/B sweeps in one process)
+  if (!w.order || simds <= 0 || w.Bt <= simds || !env) return 0;
+  int h = atoi(env);
+  if (h < 0) h = 0;
+  if (h > simds / 2) h = simds / 2;
+  return h < w.Bt ? h : 0;
+}
+
+template <int KIND, int NX, int NU>
+static hipError_t solve_split(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                              double bp0, int max_solves, size_t lds, hipStream_t s, int heavy) {
+  thread_local hipStream_t s2 = nullptr;
+  thread_local hipEvent_t fork = nullptr, join = nullptr;
+  if (!s2) {
+    if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess) return hipErrorUnknown;
+    if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess) return hipErrorUnknown;
+    if (hipEventCreateWithFlags(&join, hipEventDisableTiming) != hipSuccess) return hipErrorUnknown;
+  }
+  hipError_t e;
+  if ((e = hipEventRecord(fork, s)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(s2, fork, 0)) != hipSuccess) return e;
+  // the heavy launch first, so its workgroups are placed before the two-wave ones fill the SIMDs
+  if ((e = solve_w<KIND, NX, NU, 1>(p, w, mode, terminal, bp0, max_solves, lds, s, heavy)) != hipSuccess)
+    return e;
+  noc_ipm_ws rest = w;
+  rest.order = w.order + heavy;
+  if ((e = solve_w<KIND, NX, NU, 2>(p, rest, mode, terminal, bp0, max_solves, lds, s2, w.Bt - heavy)) !=
+      hipSuccess)
+    return e;
+  if ((e = hipEventRecord(join, s2)) != hipSuccess) return e;
+  return hipStreamWaitEvent(s, join, 0);
 }
 
 template <int KIND, int NX, int NU>
@@ -689,6 +725,8 @@ static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, in
     static const char* env = getenv("NOC_PERSIST_WAVES");
     const bool one = env ? atoi(env) == 1 : (simds > 0 && w.Bt <= simds);
     if (one) return solve_w<KIND, NX, NU, 1>(p, w, mode, terminal, bp0, max_solves, lds, s);
+    const int heavy = env ? 0 : heavy_count(w, simds);
+    if (heavy > 0) return solve_split<KIND, NX, NU>(p, w, mode, terminal, bp0, max_solves, lds, s, heavy);
   }
   return solve_w<KIND, NX, NU, 2>(p, w, mode, terminal, bp0, max_solves, lds, s);
 }

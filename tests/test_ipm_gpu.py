@@ -429,6 +429,30 @@ def test_wide_solve_matches_one_wave_kernel(name, N, Bt, mode, monkeypatch):
         assert np.max(np.abs(Uw[b] - Un[b])) <= 1e-6 * max(1.0, float(np.max(np.abs(Un))))
 
 
+@pytest.mark.parametrize("heavy", ["1", "64"])
+def test_heavy_first_split_gives_identical_results(heavy, monkeypatch):
+    """The probe-ordered resume of a batch larger than one wave per SIMD with its first `heavy`
+    launch-order entries on the one-wave instance and the rest on the two-wave instance,
+    concurrently on two streams (NOC_PERSIST_HEAVY, ipm_persistent.hip: solve_split): every
+    trajectory's controls, states and counters are bit-identical to the single two-wave launch."""
+    monkeypatch.setenv("NOC_PERSIST_WIDE", "0")
+    from noc.ipm import BatchedIPM
+    simds = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    N, Bt = 30, simds + 77   # beyond one wave per SIMD: the two-wave instance, split engaged
+    ocp, x0, u0 = _resume_case("cartpole", N, Bt, seed=6)
+    keys = ("u", "x", "kkt_solves", "total_it", "phase", "bp", "rp", "rinc", "repeats")
+    res = {}
+    for h in ("0", heavy):
+        monkeypatch.setenv("NOC_PERSIST_HEAVY", h)
+        eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
+        eng.load(u0, x0)
+        eng.solve_persistent(schedule="probe")
+        torch.cuda.synchronize()
+        res[h] = {k: eng.t[k].cpu().numpy().copy() for k in keys}
+    for k in keys:
+        assert np.array_equal(res["0"][k], res[heavy][k]), k
+
+
 def test_rp_update_rounds_like_the_reference():
     """The regularisation update after an accepted step, rp * max(1/3, 1 - (2 gain - 1) ** 3)
     (P:167-173, S:139-143), rounds like the reference: the cube as lax.integer_pow, c * (c * c),
