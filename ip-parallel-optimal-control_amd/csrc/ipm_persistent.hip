@@ -29,7 +29,7 @@ namespace noc {
 // Per-phase cycle counters of workgroup 0 (timing-only instrumentation; built only with
 // -DNOC_PERSIST_PROFILE, read back by noc_debug_phase_cycles): rollout, linearise, costate +
 // blocks, KKT scan, trial, number of Newton iterations.
-__device__ long long g_phase_cycles[8];
+__device__ long long g_phase_cycles[8];  // [6]: the trial's costs + reductions; [7]: the costate scan
 // Start / end wall-clock stamps (s_memrealtime, 100 MHz) of every trajectory's persistent solve,
 // same builds only (read back by noc_debug_traj_times): the batch's schedule, e.g. when the
 // straggler that sets the wall time started and how its neighbours thinned out.
@@ -118,8 +118,13 @@ struct CompactSrc {
 
 #ifdef NOC_PERSIST_PROFILE
 #define NOC_PHASE(i) do { const long long t_ = clock64(); if (b == 0 && l == 0) g_phase_cycles[i] += t_ - t_prev; t_prev = t_; } while (0)
+// a sub-phase ending now, started at t0 (does not move t_prev)
+#define NOC_SUB(i, t0) do { if (b == 0 && l == 0) g_phase_cycles[i] += clock64() - (t0); } while (0)
+#define NOC_T0(v) const long long v = clock64()
 #else
 #define NOC_PHASE(i) do { } while (0)
+#define NOC_SUB(i, t0) do { } while (0)
+#define NOC_T0(v) do { } while (0)
 #endif
 
 // WPS: waves per SIMD the register budget is sized for.  2 = 256 registers per lane; 1 = 512, the
@@ -314,6 +319,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         NOC_PHASE(1);
         const double* xN = X + (size_t)N * NX;
         double lamN[NX];
+        NOC_T0(t_cs);
         f.final_grad(xN, lamN);  // grad(final_cost) (C:35)
         if (last) {
           NOC_UNROLL for (int i = 0; i < NX; ++i) {
@@ -347,6 +353,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         double lam[NX];
         shfl_down_arr<NX>(g.v, lam, 1, PL);
         if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) lam[i] = lamN[i];
+        NOC_SUB(7, t_cs);
         double csum = 0.0, hmax = 0.0, g2s = 0.0;
         // One stage of the costate sweep fused with its LQ blocks.  `valid` = false computes on a
         // clamped duplicate stage and leaves lambda, the sums and memory untouched (selects, not
@@ -492,6 +499,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       const bool bwd_ok = w.feasible[b] != 0;
       NOC_PHASE(3);
       // ---------------- trial point (P:156-175 / S:121-161) ----------------
+      NOC_T0(t_tr);
       double tsum = 0.0;
       int ok = 1;
       auto trial_load = [&](int k, double* xt, double* ut) {
@@ -526,6 +534,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       }
       tsum = wave_sum(tsum);
       const bool traj_ok = __all(ok);
+      NOC_SUB(6, t_tr);
       const double new_cost = traj_ok ? tsum : INFINITY;       // P:159-163, S:126-129
       const double gain = (new_cost - cost) / pred;             // P:164-165
       const bool success = (gain > 0.0) && bwd_ok;              // P:166 / S:137
@@ -732,14 +741,20 @@ static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, in
 }
 
 int debug_phase_cycles(long long* out, int n, int reset) {
-  long long host[8];
+  long long host[8], sub[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase_cycles), sizeof(host)) != hipSuccess) return -1;
+#ifdef NOC_PERSIST_PROFILE  // the one-wave kernel's KKT sub-phases (kkt_scan_impl.h: NOC_STAMP)
+  if (hipMemcpyFromSymbol(sub, HIP_SYMBOL(g_scan_sub), sizeof(sub)) != hipSuccess) return -1;
+#endif
   long long wide[16];
   if (debug_wide_cycles(wide, 16, reset) != 0) return -1;  // the wide kernel's (ipm_wide.hip)
-  for (int i = 0; i < n && i < 16; ++i) out[i] = (i < 8 ? host[i] : 0) + wide[i];
+  for (int i = 0; i < n && i < 16; ++i) out[i] = (i < 8 ? host[i] : sub[i - 8]) + wide[i];
   if (reset) {
     const long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), zero, sizeof(zero)) != hipSuccess) return -1;
+#ifdef NOC_PERSIST_PROFILE
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_scan_sub), zero, sizeof(zero)) != hipSuccess) return -1;
+#endif
   }
   return 0;
 }

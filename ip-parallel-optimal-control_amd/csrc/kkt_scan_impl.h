@@ -55,8 +55,22 @@ __device__ long long g_scan_stamps[kStampWaves][kStampSlots][2];
       g_scan_stamps[wv_][i][1] = (long long)__builtin_amdgcn_s_memtime();                    \
     }                                                                                        \
   } while (0)
+#define NOC_STAMP_DECL do { } while (0)
+#elif defined(NOC_PERSIST_PROFILE)
+// The persistent solvers' profile build (prof_ipm_persistent.o): cycles between the scan's phase
+// boundaries for trajectory 0, lane 0, summed over its solves (noc_debug_phase_cycles slots 9-14:
+// in-chunk elements, cross-lane scan, in-chunk Riccati, forward scan, propagation, copy-out)
+static __device__ long long g_scan_sub[8];
+#define NOC_STAMP_DECL long long stamp_prev_ = 0
+#define NOC_STAMP(i)                                                                         \
+  do {                                                                                       \
+    const long long t_ = clock64();                                                          \
+    if ((i) > 0 && traj == 0 && l == 0) g_scan_sub[i] += t_ - stamp_prev_;                   \
+    stamp_prev_ = t_;                                                                        \
+  } while (0)
 #else
 #define NOC_STAMP(i) do { } while (0)
+#define NOC_STAMP_DECL do { } while (0)
 #endif
 
 // Which entries of a stage's A, B may be nonzero: the generic scan takes every one; the persistent
@@ -636,6 +650,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     abn = (CACHE == 0 && a.mode != MODE_FWD && !(a.ablate & (16 | 64))) ? a.ab_slots : 0;
     if (abn > 0) lab = lds_ab<NX, NU>(a.lds_base, a.ab_slots);
   }
+  NOC_STAMP_DECL;
   NOC_STAMP(0);
   StageData<NX, NU> cache[CACHE > 0 ? CACHE : 1];
   if constexpr (CACHE > 0) {

@@ -301,7 +301,8 @@ def test_ddp_one_stage_below_the_schedule_floor():
     from noc import problems
     from oracle import noc_oracle as O
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = json.load(open(os.path.join(root, "profiles", "r05", "ddp_flip",
+    # the envelope measured in round 5 (profiles/r05/ddp_flip/), kept with the test fixtures
+    env = json.load(open(os.path.join(root, "tests", "golden",
                                       "envelope_pendulum20_seed5_bp5e-5.json")))
     N = 20
     ocp = problems.pendulum(1.0 / N)
