@@ -21,13 +21,21 @@ namespace noc {
 
 constexpr double kTwoPi = 6.283185307179586;  // 2.0 * jnp.pi
 
-// noc/utils.py:8-10 with jnp.remainder semantics (C fmod, + divisor if the sign differs)
-// fmod(a, 2 pi) == a exactly for |a| < 2 pi, so the general fmod routine (~70 instructions, a
-// loop) only runs for lanes outside that range -- a branch, not a select, so a wave whose angles
-// all lie in (-2 pi, 2 pi) skips it.
+// noc/utils.py:8-10 with jnp.remainder semantics (C fmod, + divisor if the sign differs).
+// fmod is exact, and so is its value on the two innermost periods: fmod(a, 2 pi) == a for
+// |a| < 2 pi, and a - sign(a) 2 pi for 2 pi <= |a| < 4 pi (Sterbenz: the subtraction of two
+// doubles within a factor of two is exact, so this IS fmod's result bit for bit).  The general
+// fmod routine (a loop of ~100s of instructions) runs only beyond 4 pi, behind a branch.  The
+// cart-pole's angle lives around 2 pi (examples/cartpole_runtime.py: the pole hangs at 0 = 2 pi
+// and swings up to pi), so before round 6 every stage cost, gradient and trial point of a typical
+// trajectory took the loop -- 2/3 of the trial phase.
 NOC_DEV double wrap_angle(double a) {
   double r = a;
-  if (__builtin_expect(!(fabs(a) < kTwoPi), 0)) r = fmod(a, kTwoPi);
+  const double fa = fabs(a);
+  if (fa >= kTwoPi) {
+    if (__builtin_expect(fa < 2.0 * kTwoPi, 1)) r = a - copysign(kTwoPi, a);
+    else r = fmod(a, kTwoPi);
+  }
   return (r != 0.0 && r < 0.0) ? r + kTwoPi : r;
 }
 

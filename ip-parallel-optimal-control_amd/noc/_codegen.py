@@ -61,10 +61,12 @@ def _pymod(e):
 
 
 # device helper of the generated cost code: Python / jnp remainder (sign of the divisor); the
-# general fmod routine only outside |a| < |b|, where fmod(a, b) == a exactly
+# general fmod routine only outside |a| < 2 |b|: fmod(a, b) == a exactly for |a| < |b| and
+# a - sign(a) |b| exactly for |b| <= |a| < 2 |b| (Sterbenz), fmod's own result bit for bit
 PYMOD_DEVICE = """NOC_DEV double noc_pymod(double a, double b) {
   double r = a;
-  if (!(fabs(a) < fabs(b))) r = fmod(a, b);
+  const double fa = fabs(a), fb = fabs(b);
+  if (fa >= fb) r = (fa < 2.0 * fb) ? a - copysign(fb, a) : fmod(a, b);
   return (r != 0.0 && ((r < 0.0) != (b < 0.0))) ? r + b : r;
 }"""
 

@@ -110,3 +110,23 @@ def test_traced_cost_header_compiles_into_a_family_header():
     assert "constexpr bool kCustomCost = true;" in h
     h0 = families.generate_header("ap", CF.actuated_pendulum_ode, 3, 1, False)
     assert "constexpr bool kCustomCost = false;" in h0 and "custom_feasible(" in h0
+
+
+def test_wrap_fast_path_is_fmod_bit_for_bit():
+    """The devices' wrap_angle (csrc/ipm_family.h) and noc_pymod (noc/_codegen.py) skip the fmod
+    routine on the two innermost periods: for |b| <= |a| < 2 |b|, fmod(a, b) == a - sign(a) |b|
+    exactly (Sterbenz), which is what they compute there.  Checked against C fmod (np.fmod) on
+    angles around 2 pi -- where the cart-pole's theta lives -- and on random divisors."""
+    import numpy as np
+    rng = np.random.default_rng(0)
+    two_pi = 6.283185307179586
+    a = np.concatenate([two_pi + rng.uniform(-1e-3, 1e-3, 20000), rng.uniform(two_pi, 2 * two_pi, 20000),
+                        np.nextafter(2 * two_pi, 0.0) * np.ones(1), two_pi * np.ones(1)])
+    for s in (1.0, -1.0):
+        x = s * a
+        m = np.abs(x) >= two_pi
+        assert np.array_equal((x - np.copysign(two_pi, x))[m], np.fmod(x, two_pi)[m])
+    b = rng.uniform(0.1, 10.0, 20000) * rng.choice([-1.0, 1.0], 20000)
+    a = np.abs(b) * rng.uniform(1.0, 2.0, 20000) * rng.choice([-1.0, 1.0], 20000)
+    ok = np.abs(a) < 2 * np.abs(b)
+    assert np.array_equal((a - np.copysign(np.abs(b), a))[ok], np.fmod(a, b)[ok])
