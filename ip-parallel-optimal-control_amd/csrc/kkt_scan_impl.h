@@ -615,13 +615,9 @@ struct ArgsSrc {
 // LDS per wave): A, B of chunk slots j < a.ab_slots stay in LDS from phase 1 to phases 3 and 4
 // (lds_ab); a.ab_slots = 0 turns it off at run time.  Not in the two-wave segments (L = 128): their
 // re-reads are L2 hits already, and the slots measured +2.5 % there (profiles/r05/ab_slots/).
-// PF: phases 1 and 3 load stage s-1's blocks while stage s is computed (one stage in flight; the
-// persistent solver's compact blocks are 12 doubles per cart-pole stage, so the second copy is
-// cheap in registers -- for the dense blocks it spilled).  Not with AB or CACHE.
 template <int NX, int NU, int L, bool AFF, bool TILED, class SRC, int CACHE = 0, bool HANDOFF = true,
-          bool BIG = false, bool NT3 = false, bool AB = (BIG && ab_supported<NX, NU>()), bool PF = false>
+          bool BIG = false, bool NT3 = false, bool AB = (BIG && ab_supported<NX, NU>())>
 NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, const SRC& src) {
-  static_assert(!PF || (!AB && CACHE == 0), "the prefetched loops replace the plain ones only");
   constexpr int KD = kd_width<NX, NU>();
   using ST = typename SRC::Struct;  // structural zeros of A, B (DenseBlocks: none)
   if (traj >= a.B) return;                     // uniform over the segment
@@ -695,14 +691,6 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     if constexpr (CACHE > 0) {
       NOC_UNROLL for (int jj = CACHE - 1; jj >= 0; --jj)
         if (jj < len) prepend<NX, NU, AFF, ST>(e, cache[jj], reg);
-    } else if constexpr (PF) {
-      StageData<NX, NU> nxt;
-      if (len > 0) src.stage(start + len - 1, len - 1, reg, nxt);
-      for (int s = start + len - 1; s >= start; --s) {
-        const StageData<NX, NU> st = nxt;
-        if (s > start) src.stage(s - 1, s - 1 - start, reg, nxt);  // in flight during the prepend
-        prepend<NX, NU, AFF, ST>(e, st, reg);
-      }
     } else {
       for (int s = start + len - 1; s >= start; --s) {
         StageData<NX, NU> st;
@@ -906,22 +894,6 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
             ab_load<NX, NU>(lab, s - start, st.A, st.B);
             riccati_stage(s, st);
           }
-        }
-      } else if constexpr (HANDOFF && PF) {
-        StageData<NX, NU> nxt;
-        if (len > 0) stage3(start + len - 1, nxt);
-        for (int s = start + len - 1; s > start; --s) {
-          const StageData<NX, NU> st = nxt;
-          stage3(s - 1, nxt);  // in flight during this stage's Riccati step
-          riccati_stage(s, st);
-        }
-        if (len > 0) {  // the chunk's first stage (already loaded): its A, B (c) go on to phase 4
-          const StageData<NX, NU> st = nxt;
-          riccati_stage(start, st);
-          hA = st.A;
-          hB = st.B;
-          if constexpr (AFF) hc = st.c; else set_zero(hc);
-          handed = a.mode == MODE_FULL && !(a.ablate & 32);
         }
       } else if constexpr (HANDOFF) {
         for (int s = start + len - 1; s > start; --s) {

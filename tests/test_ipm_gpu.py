@@ -353,8 +353,10 @@ def test_multilaunch_max_steps_caps_running_trajectories():
     ("cartpole", 300, 3, "par"),     # N > 256: two stages on some lanes
     ("linear2", 100, 5, "par"),
 ])
-def test_wide_solve_matches_one_wave_kernel(name, N, Bt, mode, monkeypatch):
-    """The wide whole-solve kernel (ipm_wide.hip: four waves per trajectory, blocks in LDS) against
+@pytest.mark.parametrize("waves", ["4", "2"])
+def test_wide_solve_matches_one_wave_kernel(name, N, Bt, mode, waves, monkeypatch):
+    """The wide whole-solve kernel (ipm_wide.hip: four -- or, NOC_WIDE_WAVES=2, two -- waves per
+    trajectory, compact blocks in LDS) against
     the one-wave kernel on the same inputs: identical outer iterations per trajectory, identical
     KKT solves and controls within 1e-8 relative (the scans associate differently, so not
     bit-identical) -- except where an accept test (P:159-173) is decided below the resolution of
@@ -384,6 +386,7 @@ def test_wide_solve_matches_one_wave_kernel(name, N, Bt, mode, monkeypatch):
         ocp = problems.make_problem(name, N)
         x0, u0 = problems.initial_conditions(name, N, Bt, seed=33)
     m = _lib.MODE_PAR if mode == "par" else _lib.MODE_SEQ
+    monkeypatch.setenv("NOC_WIDE_WAVES", waves)
     res = []
     for wide in ("1", "0"):
         monkeypatch.setenv("NOC_PERSIST_WIDE", wide)
@@ -406,7 +409,7 @@ def test_wide_solve_matches_one_wave_kernel(name, N, Bt, mode, monkeypatch):
     assert os.path.exists(tlib), "decision-trace build missing (make trace-lib / build())"
     eps = np.finfo(np.float64).eps
     for b in np.flatnonzero(flip):
-        out = os.path.join(root, "gpurun_out", f"flip_{name}_{N}_{mode}_{b}.json")
+        out = os.path.join(root, "gpurun_out", f"flip_{name}_{N}_{mode}_{b}_w{waves}.json")
         os.makedirs(os.path.dirname(out), exist_ok=True)
         env = dict(os.environ, NOC_HIP_LIB=tlib)
         env.pop("NOC_PERSIST_WIDE", None)
