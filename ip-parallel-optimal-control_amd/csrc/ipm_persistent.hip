@@ -24,8 +24,8 @@
 #include "kkt_scan_impl.h"
 #include "noc_internal.h"
 
-#ifndef NOC_PERSIST_MASKED
-#define NOC_PERSIST_MASKED 1
+#ifndef NOC_PERSIST_PF
+#define NOC_PERSIST_PF 1
 #endif
 
 namespace noc {
@@ -491,12 +491,10 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       // traffic -- c3 ipm_solve -2.4 %, c2 -1 %, bit-identical (profiles/r05/handoff_persist/)
       {
         const CompactSrc<BS, NX, NU, PL> src{a, prm, b, l, cmax, (size_t)b * N};
-        // BIG = masked combines (no identity partner, no per-dword selects) where the instance
-        // owns its SIMD (512 registers) -- NOC_PERSIST_MASKED: 0 never, 1 at one wave per SIMD
-        // (default), 2 always (a build switch for the A/B)
-        constexpr bool MASK = NOC_PERSIST_MASKED == 2 || (NOC_PERSIST_MASKED == 1 && WPS == 1);
-        kkt_scan_wave_src<NX, NU, PL, false, true, CompactSrc<BS, NX, NU, PL>, 0, true, MASK, false,
-                          false>(a, b, l, src);
+        // PF: phases 1 / 3 keep one stage's compact blocks in flight (NOC_PERSIST_PF, a build
+        // switch for the A/B)
+        kkt_scan_wave_src<NX, NU, PL, false, true, CompactSrc<BS, NX, NU, PL>, 0, true, false, false,
+                          false, STRUCT && NOC_PERSIST_PF != 0>(a, b, l, src);
       }
       wave_fence();  // pred / feasible written by lane 0
       {
