@@ -24,10 +24,6 @@
 #include "kkt_scan_impl.h"
 #include "noc_internal.h"
 
-#ifndef NOC_PERSIST_PF
-#define NOC_PERSIST_PF 1
-#endif
-
 namespace noc {
 
 // Per-phase cycle counters of workgroup 0 (timing-only instrumentation; built only with
@@ -491,10 +487,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       // traffic -- c3 ipm_solve -2.4 %, c2 -1 %, bit-identical (profiles/r05/handoff_persist/)
       {
         const CompactSrc<BS, NX, NU, PL> src{a, prm, b, l, cmax, (size_t)b * N};
-        // PF: phases 1 / 3 keep one stage's compact blocks in flight (NOC_PERSIST_PF, a build
-        // switch for the A/B)
-        kkt_scan_wave_src<NX, NU, PL, false, true, CompactSrc<BS, NX, NU, PL>, 0, true, false, false,
-                          false, STRUCT && NOC_PERSIST_PF != 0>(a, b, l, src);
+        kkt_scan_wave_src<NX, NU, PL, false, true, CompactSrc<BS, NX, NU, PL>, 0, true>(a, b, l, src);
       }
       wave_fence();  // pred / feasible written by lane 0
       {
