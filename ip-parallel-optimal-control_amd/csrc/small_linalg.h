@@ -82,13 +82,27 @@ NOC_DEV void gstore(double* __restrict__ dst, const double* src) {
   }
 }
 
-// load a full row-major N x N matrix and symmetrise it into packed storage
+// A value the compiler cannot see into: a product kept as its own rounded result.  The KKT scan
+// units are built with -ffp-contract=fast, under which the backend may fuse ANY multiply into a
+// following add, whatever the source's pragmas -- and it chooses per inlined copy.
+NOC_DEV double opaque(double v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// load a full row-major N x N matrix and symmetrise it into packed storage.  The off-diagonal
+// 0.5 (a + b) is opaque: a symmetrised Q(i, j) starts the Riccati sums S = Q + A'SA + ..., and
+// two inlined copies of that step fused it differently -- fma(0.5, a + b, A * SA) in one,
+// 0.5 (a + b) rounded then fma(A, SA, .) in the other (round 6 ISA: six v_fmac_f64 with 0.5 in
+// the A, B-slot path's phase 3, six v_mul_f64 by 0.5 in the re-read path's), so the natural
+// layout's results depended on which path the batch size selected (tests/test_kkt_gpu.py:
+// test_ab_slots_equal_rereads).  Now both round the symmetrised entry first.
 template <int N>
 NOC_DEV void gload_sym(const double* __restrict__ src, Sym<N>& S) {
   double t[N * N];
   gload<N * N>(src, t);
   NOC_UNROLL for (int i = 0; i < N; ++i)
-    NOC_UNROLL for (int j = i; j < N; ++j) S(i, j) = (i == j) ? t[i * N + i] : 0.5 * (t[i * N + j] + t[j * N + i]);
+    NOC_UNROLL for (int j = i; j < N; ++j) S(i, j) = (i == j) ? t[i * N + i] : opaque(0.5 * (t[i * N + j] + t[j * N + i]));
 }
 template <int N>
 NOC_DEV void gstore_sym(double* __restrict__ dst, const Sym<N>& S) {
