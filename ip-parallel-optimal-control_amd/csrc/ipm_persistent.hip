@@ -49,10 +49,29 @@ struct IpmState {
   double bp, rp, rinc, cost, hu, gnorm;
   int it, inner, total_it, solves;
 };
+// Speculative candidates (SPEC > 1 waves per trajectory, one candidate regularisation each): the
+// scan's reg / pred / feasible of a wave's candidate, and its trial cost, exchanged through LDS.
+struct SpecIO {
+  double reg, pred, new_cost, pad;
+  int feasible, pad2[3];
+};
+
+// LDS of one workgroup, in doubles: SPEC regions of KKT slots (lds_slots: one per 64-lane
+// segment), SPEC parked states, SPEC SpecIO records (SPEC > 1 only), then SPEC copies of x, u
+// (XLDS).  SPEC = 1 is the one-wave layout: [slots][state][x, u].
 template <int NX, int NU>
-NOC_DEV IpmState* state_slot(int N) {
+__host__ __device__ constexpr int slot_doubles(int N) { return (N * kd_width<NX, NU>() + NX + 1) & ~1; }
+__host__ __device__ constexpr int state_doubles() { return (int)((sizeof(IpmState) + 15) / 16) * 2; }
+__host__ __device__ constexpr int specio_doubles(int spec) { return spec > 1 ? (int)(sizeof(SpecIO) / 8) * spec : 0; }
+template <int NX, int NU>
+NOC_DEV IpmState* state_slot(int N, int spec = 1, int wv = 0) {
   extern __shared__ __attribute__((aligned(16))) double noc_smem[];
-  return reinterpret_cast<IpmState*>(noc_smem + ((N * kd_width<NX, NU>() + NX + 1) & ~1));
+  return reinterpret_cast<IpmState*>(noc_smem + spec * slot_doubles<NX, NU>(N) + wv * state_doubles());
+}
+template <int NX, int NU>
+NOC_DEV SpecIO* spec_io(int N, int spec, int wv) {
+  extern __shared__ __attribute__((aligned(16))) double noc_smem[];
+  return reinterpret_cast<SpecIO*>(noc_smem + spec * (slot_doubles<NX, NU>(N) + state_doubles())) + wv;
 }
 
 // XLDS instances: the trajectory's states and controls x[0..N], u[0..N-1] live in LDS for the
@@ -60,11 +79,11 @@ NOC_DEV IpmState* state_slot(int N) {
 // them; from the workspace each access was a global round trip), copied in at the start and out
 // at the end.  Layout behind the KKT slots and the parked state: x [(N+1) NX], u [N NU].
 template <int NX, int NU>
-NOC_DEV constexpr int xlds_off(int N) {
-  return ((N * kd_width<NX, NU>() + NX + 1) & ~1) + (int)((sizeof(IpmState) + 15) / 16) * 2;
-}
+__host__ __device__ constexpr int xlds_doubles(int N) { return ((N + 1) * NX + N * NU + 1) & ~1; }
 template <int NX, int NU>
-NOC_DEV constexpr int xlds_doubles(int N) { return ((N + 1) * NX + N * NU + 1) & ~1; }
+__host__ __device__ constexpr int xlds_off(int N, int spec = 1, int wv = 0) {
+  return spec * (slot_doubles<NX, NU>(N) + state_doubles()) + specio_doubles(spec) + wv * xlds_doubles<NX, NU>(N);
+}
 
 // The KKT scan's block source in the persistent solver: the workspace's compact tiled fields (only
 // the variable entries of A, B, Q, R, M; block_struct.h), expanded with the family's constants as
@@ -117,9 +136,9 @@ struct CompactSrc {
 }  // namespace
 
 #ifdef NOC_PERSIST_PROFILE
-#define NOC_PHASE(i) do { const long long t_ = clock64(); if (b == 0 && l == 0) g_phase_cycles[i] += t_ - t_prev; t_prev = t_; } while (0)
+#define NOC_PHASE(i) do { const long long t_ = clock64(); if (b == 0 && lead) g_phase_cycles[i] += t_ - t_prev; t_prev = t_; } while (0)
 // a sub-phase ending now, started at t0 (does not move t_prev)
-#define NOC_SUB(i, t0) do { if (b == 0 && l == 0) g_phase_cycles[i] += clock64() - (t0); } while (0)
+#define NOC_SUB(i, t0) do { if (b == 0 && lead) g_phase_cycles[i] += clock64() - (t0); } while (0)
 #define NOC_T0(v) const long long v = clock64()
 #else
 #define NOC_PHASE(i) do { } while (0)
@@ -134,13 +153,21 @@ struct CompactSrc {
 // register allocation does not carry the resume bookkeeping).
 // STRUCT: the structure-aware blocks (block_struct.h; NOC_PERSIST_STRUCT=0 selects the dense
 // instance, which computes the same doubles).
-template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS, bool STRUCT>
-__global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
-                                                         int terminal, double bp0,
-                                                         int max_solves) {
-  // one wave (= one 64-thread workgroup) per trajectory; w.order: the launch order (a permutation)
+// SPEC: waves per trajectory, each solving one candidate of the regularisation's failure chain
+// (speculative retries, below); 1 = the plain solver.  SPEC > 1 needs XLDS (every wave keeps its
+// own copy of x, u) and runs no RESUME launch.
+template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS, bool STRUCT, int SPEC = 1>
+__global__ __launch_bounds__(64 * SPEC, WPS) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
+                                                                int terminal, double bp0,
+                                                                int max_solves) {
+  static_assert(SPEC == 1 || (XLDS && !RESUME), "speculative waves keep x, u in LDS, no resume");
+  // one wave (= one 64-thread workgroup) per trajectory -- SPEC waves with SPEC > 1; w.order: the
+  // launch order (a permutation)
   const int b = w.order ? w.order[blockIdx.x] : (int)blockIdx.x;
-  const int l = threadIdx.x;
+  const int l = SPEC > 1 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;  // lane = chunk owner
+  const int wv = SPEC > 1 ? (int)(threadIdx.x >> 6) : 0;                 // candidate of this wave
+  const bool lead = (l == 0) && (wv == 0);  // writes the trajectory's results
+  (void)lead;
   if (b < 0 || b >= w.Bt) return;  // an out-of-range order entry solves nothing (never faults)
   constexpr int KD = kd_width<NX, NU>();
   Fam<KIND, NX, NU> f(prm);
@@ -161,8 +188,8 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
   double* const Xg = w.x + (size_t)b * (N + 1) * NX;
   double* const Ug = w.u + (size_t)b * N * NU;
   extern __shared__ __attribute__((aligned(16))) double noc_smem[];
-  double* const X = XLDS ? noc_smem + xlds_off<NX, NU>(N) : Xg;
-  double* const U = XLDS ? noc_smem + xlds_off<NX, NU>(N) + (N + 1) * NX : Ug;
+  double* const X = XLDS ? noc_smem + xlds_off<NX, NU>(N, SPEC, wv) : Xg;
+  double* const U = XLDS ? noc_smem + xlds_off<NX, NU>(N, SPEC, wv) + (N + 1) * NX : Ug;
   if constexpr (XLDS) {  // the workspace's x (a resume point's states) and u into LDS
     for (int i = l; i < (N + 1) * NX; i += 64) X[i] = Xg[i];
     for (int i = l; i < N * NU; i += 64) U[i] = Ug[i];
@@ -178,6 +205,12 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
   a.pred = w.pred; a.feasible = w.feasible;
   a.tiled = 1;
   a.lds_out = 1;  // dx, du stay in LDS (a.dx = a.du = NULL): the trial reads them there
+  SpecIO* const io = SPEC > 1 ? spec_io<NX, NU>(N, SPEC, wv) : nullptr;
+  if constexpr (SPEC > 1) {  // this wave's candidate: reg, pred, feasible in its LDS record
+    a.reg = &io->reg;
+    a.pred = &io->pred;
+    a.feasible = &io->feasible;
+  }
 
   double bp = bp0, rp = 1.0, rinc = 2.0, cost = 0.0, hu = 1.0, gnorm = 0.0;
   int it = 0, inner = 0, total_it = 0, solves = 0;
@@ -190,12 +223,12 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
     solves = w.kkt_solves[b]; entry = resume_phase(w.phase[b]);
     if (entry == NOC_PHASE_DONE) return;  // uniform over the wave
   } else {
-    if (l == 0 && w.repeats) w.repeats[b] = 0;
+    if (lead && w.repeats) w.repeats[b] = 0;
   }
 
 #ifdef NOC_PERSIST_PROFILE
   long long t_prev = clock64();
-  if (l == 0 && b < kTrajStamps) g_traj_times[b][0] = (long long)__builtin_amdgcn_s_memrealtime();
+  if (lead && b < kTrajStamps) g_traj_times[b][0] = (long long)__builtin_amdgcn_s_memrealtime();
 #endif
   // lc_fresh: the workspace's stage costs (w.lc) already belong to the current (x, u) -- the last
   // trial wrote them, and it was taken -- so the next linearisation skips f.stage_cost (the
@@ -468,16 +501,35 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
         }
         keep_state = false;
         // regularisation: par R += rp*||cu||*I (P:116-118); seq Quu += mu*I (S:51)
-        const double reg = (mode == NOC_MODE_PAR) ? rp * gnorm : rp;
-        w.reg[b] = reg;  // every lane stores the same value and reads its own store back
         relinearize = false;
+      }
+      // The candidates of this solve: candidate k is the regularisation the solver reaches after
+      // k rejected trials at this point (P:167-173 / S:139-144).  SPEC = 1: only k = 0, stored per
+      // trajectory as before; SPEC > 1: wave k solves candidate k (its LDS record).
+      double c_reg[SPEC];
+      {
+        double r = rp, ri = rinc;
+        NOC_UNROLL for (int k = 0; k < SPEC; ++k) {
+          c_reg[k] = (mode == NOC_MODE_PAR) ? r * gnorm : r;
+          r = r * ri;
+          ri = 2.0 * ri;
+          if (mode == NOC_MODE_PAR) r = fmin(fmax(r, 1e-16), 1e16);
+        }
+      }
+      if constexpr (SPEC == 1) {
+        w.reg[b] = c_reg[0];  // every lane stores the same value and reads its own store back
       } else {
-        w.reg[b] = (mode == NOC_MODE_PAR) ? rp * gnorm : rp;
+        double rw = c_reg[0];
+        NOC_UNROLL for (int k = 1; k < SPEC; ++k) rw = (wv == k) ? c_reg[k] : rw;
+        io->reg = rw;
       }
       NOC_PHASE(2);
       wave_fence();  // the terminal Hessian (stage-0 lane) and the blocks before the scan
+      // SPEC > 1: every wave has written the blocks (the same doubles) and read w.lc before any
+      // wave's trial overwrites w.lc
+      if constexpr (SPEC > 1) __syncthreads();
       {  // park the state (every lane stores the same values)
-        IpmState* st = state_slot<NX, NU>(N);
+        IpmState* st = state_slot<NX, NU>(N, SPEC, wv);
         st->bp = bp; st->rp = rp; st->rinc = rinc; st->cost = cost; st->hu = hu; st->gnorm = gnorm;
         st->it = it; st->inner = inner; st->total_it = total_it; st->solves = solves;
       }
@@ -487,21 +539,23 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       // traffic -- c3 ipm_solve -2.4 %, c2 -1 %, bit-identical (profiles/r05/handoff_persist/)
       {
         const CompactSrc<BS, NX, NU, PL> src{a, prm, b, l, cmax, (size_t)b * N};
-        kkt_scan_wave_src<NX, NU, PL, false, true, CompactSrc<BS, NX, NU, PL>, 0, true>(a, b, l, src);
+        kkt_scan_wave_src<NX, NU, PL, false, true, CompactSrc<BS, NX, NU, PL>, 0, true, false, false, false,
+                          (SPEC > 1)>(a, b, l, src);
       }
       wave_fence();  // pred / feasible written by lane 0
       {
-        const IpmState* st = state_slot<NX, NU>(N);
+        const IpmState* st = state_slot<NX, NU>(N, SPEC, wv);
         bp = st->bp; rp = st->rp; rinc = st->rinc; cost = st->cost; hu = st->hu; gnorm = st->gnorm;
         it = st->it; inner = st->inner; total_it = st->total_it; solves = st->solves;
       }
-      const double pred = w.pred[b];
-      const bool bwd_ok = w.feasible[b] != 0;
       NOC_PHASE(3);
       // ---------------- trial point (P:156-175 / S:121-161) ----------------
+      // (SPEC > 1: wave 0's trial costs go to w.lc -- the next linearisation's if its candidate is
+      // taken; the other waves' are recomputed there, the same doubles)
       NOC_T0(t_tr);
       double tsum = 0.0;
       int ok = 1;
+      const bool lc_out = SPEC == 1 || wv == 0;
       auto trial_load = [&](int k, double* xt, double* ut) {
         NOC_UNROLL for (int i = 0; i < NX; ++i) xt[i] = X[(size_t)k * NX + i] + slot[k * KD + i];
         NOC_UNROLL for (int jj = 0; jj < NU; ++jj) ut[jj] = U[(size_t)k * NU + jj] + slot[k * KD + NX + jj];
@@ -514,8 +568,8 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
           const double c0 = f.stage_cost(xt0, ut0, bp);
           const double c1 = f.stage_cost(xt1, ut1, bp);
           const bool f0 = f.feasible(xt0, ut0), f1 = f.feasible(xt1, ut1);
-          if (j < len) { ok &= f0 ? 1 : 0; tsum += c0; tstore<1, PL>(w.lc, b, j, l, cmax, &c0); }
-          if (j + 1 < len) { ok &= f1 ? 1 : 0; tsum += c1; tstore<1, PL>(w.lc, b, j + 1, l, cmax, &c1); }
+          if (j < len) { ok &= f0 ? 1 : 0; tsum += c0; if (lc_out) tstore<1, PL>(w.lc, b, j, l, cmax, &c0); }
+          if (j + 1 < len) { ok &= f1 ? 1 : 0; tsum += c1; if (lc_out) tstore<1, PL>(w.lc, b, j + 1, l, cmax, &c1); }
         }
       } else {
         for (int j = 0; j < len; ++j) {
@@ -524,7 +578,7 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
           ok &= f.feasible(xt, ut) ? 1 : 0;
           const double c = f.stage_cost(xt, ut, bp);
           tsum += c;
-          tstore<1, PL>(w.lc, b, j, l, cmax, &c);  // the next linearisation's, if taken
+          if (lc_out) tstore<1, PL>(w.lc, b, j, l, cmax, &c);  // the next linearisation's, if taken
         }
       }
       if (last) {
@@ -535,81 +589,117 @@ __global__ __launch_bounds__(64, WPS) void ipm_solve_kernel(noc_family prm, noc_
       tsum = wave_sum(tsum);
       const bool traj_ok = __all(ok);
       NOC_SUB(6, t_tr);
-      const double new_cost = traj_ok ? tsum : INFINITY;       // P:159-163, S:126-129
-      const double gain = (new_cost - cost) / pred;             // P:164-165
-      const bool success = (gain > 0.0) && bwd_ok;              // P:166 / S:137
+      // the candidates' outcomes: new cost (P:159-163, S:126-129), pred, backward feasibility
+      double c_new[SPEC], c_pred[SPEC];
+      bool c_bwd[SPEC];
+      if constexpr (SPEC == 1) {
+        c_new[0] = traj_ok ? tsum : INFINITY;
+        c_pred[0] = w.pred[b];
+        c_bwd[0] = w.feasible[b] != 0;
+      } else {
+        if (l == 0) io->new_cost = traj_ok ? tsum : INFINITY;
+        __syncthreads();  // every candidate's outcome in LDS
+        const SpecIO* io0 = spec_io<NX, NU>(N, SPEC, 0);
+        NOC_UNROLL for (int k = 0; k < SPEC; ++k) {
+          c_new[k] = io0[k].new_cost;
+          c_pred[k] = io0[k].pred;
+          c_bwd[k] = io0[k].feasible != 0;
+        }
+      }
+      // The accept tests in solve order.  Candidate k > 0 counts only if the solver reaches it:
+      // every earlier one rejected without ending the iteration, no stop, no cap, and its
+      // regularisation the one the sequential solver would use next (bit for bit) -- so the
+      // decisions, counters and iterates are the sequential solver's.
+      int winner = -1;
+      bool stop = false;
+      NOC_UNROLL for (int k = 0; k < SPEC; ++k) {
+        if (k > 0) {
+          const double reg_next = (mode == NOC_MODE_PAR) ? rp * gnorm : rp;
+          if (stage_done || relinearize || reg_next != c_reg[k]) break;
+        }
+        const double new_cost = c_new[k];
+        const double pred = c_pred[k];
+        const bool bwd_ok = c_bwd[k];
+        const double gain = (new_cost - cost) / pred;             // P:164-165
+        const bool success = (gain > 0.0) && bwd_ok;              // P:166 / S:137
 #ifdef NOC_DECISION_TRACE
-      if (l == 0) NOC_TRACE_DECISION(g_dtrace, b, solves, bp, it, inner, cost, new_cost, pred, gain,
+        if (lead) NOC_TRACE_DECISION(g_dtrace, b, solves, bp, it, inner, cost, new_cost, pred, gain,
                                      success, rp, rinc, hu, bwd_ok);
 #endif
-      const double shrink = rp_shrink(gain);  // P:169 / S:141 (noc_internal.h)
-      const double rp_used = rp;
-      rp = success ? rp * shrink : rp * rinc;                   // P:167-171 / S:139-143
-      rinc = success ? 2.0 : 2.0 * rinc;                        // P:172 / S:144
-      bool take, end_iter, stop;
-      inner += 1;
-      if (mode == NOC_MODE_PAR) {
-        rp = fmin(fmax(rp, 1e-16), 1e16);                       // P:173
-        // identical retries at the rp clip: accounted, not recomputed (noc_internal.h)
-        const int rep = par_retry_repeats(w, success, rp_used, rp, inner, max_solves - solves - 1);
-        if (rep > 0) {
-          inner += rep;
-          solves += rep;
-          rinc = ldexp(rinc, rep);  // r_inc doubles per retry (P:172)
-          if (l == 0 && w.repeats) w.repeats[b] += rep;
+        const double shrink = rp_shrink(gain);  // P:169 / S:141 (noc_internal.h)
+        const double rp_used = rp;
+        rp = success ? rp * shrink : rp * rinc;                   // P:167-171 / S:139-143
+        rinc = success ? 2.0 : 2.0 * rinc;                        // P:172 / S:144
+        bool take, end_iter;
+        inner += 1;
+        if (mode == NOC_MODE_PAR) {
+          rp = fmin(fmax(rp, 1e-16), 1e16);                       // P:173
+          // identical retries at the rp clip: accounted, not recomputed (noc_internal.h)
+          const int rep = par_retry_repeats(w, success, rp_used, rp, inner, max_solves - solves - 1);
+          if (rep > 0) {
+            inner += rep;
+            solves += rep;
+            rinc = ldexp(rinc, rep);  // r_inc doubles per retry (P:172)
+            if (lead && w.repeats) w.repeats[b] += rep;
+          }
+          end_iter = success || inner > 500;                      // P:177-182
+          take = end_iter;                                        // last trial kept (P:175, P:184)
+          stop = end_iter && (hu < 1e-4 || it + 1 > 1000);        // P:199-202
+        } else {
+          take = success;                                         // S:145-146
+          end_iter = true;
+          stop = (hu < 1e-4) && bwd_ok;                           // S:157-161
         }
-        end_iter = success || inner > 500;                      // P:177-182
-        take = end_iter;                                        // last trial kept (P:175, P:184)
-        stop = end_iter && (hu < 1e-4 || it + 1 > 1000);        // P:199-202
-      } else {
-        take = success;                                         // S:145-146
-        end_iter = true;
-        stop = (hu < 1e-4) && bwd_ok;                           // S:157-161
+        if (take) winner = k;
+#ifdef NOC_PERSIST_PROFILE
+        if (b == 0 && lead) g_phase_cycles[5] += 1;
+#endif
+        solves += 1;
+        it += end_iter ? 1 : 0;
+        if (stop) {                                               // barrier stage finished
+          total_it += it;                                         // P:239 / S:187
+          bp = bp / 5.0;                                          // P:238 / S:186
+          it = 0;
+          rp = 1.0;                                               // P:134 / S:110
+          rinc = 2.0;                                             // P:135 / S:111
+          stage_done = true;
+        } else if (mode == NOC_MODE_PAR) {
+          relinearize = end_iter;
+        } else {
+          relinearize = success;  // a rejected seq step only changes the regularisation
+        }
+        if (solves >= max_solves) {  // capped: record where a later launch continues
+          capped = true;
+          phase = stage_done ? NOC_PHASE_ROLLOUT : (relinearize ? NOC_PHASE_LINEARIZE : NOC_PHASE_SOLVE);
+          if (stage_done && (!(bp > 1e-4) || (w.flags & NOC_WS_ONE_STAGE))) phase = NOC_PHASE_DONE;
+          break;
+        }
       }
-      if (take) {  // x <- x + dx, u <- u + du on the own chunk (its later readers are this lane)
+      if (winner >= 0) {  // x <- x + dx, u <- u + du on the own chunk (its later readers are this lane)
+        const double* ws = slot + (winner - wv) * slot_doubles<NX, NU>(N);  // the winner's slots
         for (int j = 0; j < len; ++j) {
           const int k = start + j;
-          NOC_UNROLL for (int i = 0; i < NX; ++i) X[(size_t)k * NX + i] += slot[k * KD + i];
-          NOC_UNROLL for (int jj = 0; jj < NU; ++jj) U[(size_t)k * NU + jj] += slot[k * KD + NX + jj];
+          NOC_UNROLL for (int i = 0; i < NX; ++i) X[(size_t)k * NX + i] += ws[k * KD + i];
+          NOC_UNROLL for (int jj = 0; jj < NU; ++jj) U[(size_t)k * NU + jj] += ws[k * KD + NX + jj];
         }
-        if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) X[(size_t)N * NX + i] += slot[N * KD + i];
+        if (last) NOC_UNROLL for (int i = 0; i < NX; ++i) X[(size_t)N * NX + i] += ws[N * KD + i];
       }
-      lc_fresh = take;  // uniform; the trial stored this point's stage costs in w.lc
+      lc_fresh = winner == 0;  // uniform; candidate 0's trial stored this point's stage costs in w.lc
       __syncthreads();  // the next KKT solve overwrites the LDS slots read above
       NOC_PHASE(4);
-#ifdef NOC_PERSIST_PROFILE
-      if (b == 0 && l == 0) g_phase_cycles[5] += 1;
-#endif
-      solves += 1;
-      it += end_iter ? 1 : 0;
-      if (stop) {                                               // barrier stage finished
-        total_it += it;                                         // P:239 / S:187
-        bp = bp / 5.0;                                          // P:238 / S:186
-        it = 0;
-        rp = 1.0;                                               // P:134 / S:110
-        rinc = 2.0;                                             // P:135 / S:111
-        stage_done = true;
-      } else if (mode == NOC_MODE_PAR) {
-        relinearize = end_iter;
-      } else {
-        relinearize = success;  // a rejected seq step only changes the regularisation
-      }
-      if (solves >= max_solves) {  // capped: record where a later launch continues
-        capped = true;
-        phase = stage_done ? NOC_PHASE_ROLLOUT : (relinearize ? NOC_PHASE_LINEARIZE : NOC_PHASE_SOLVE);
-        if (stage_done && (!(bp > 1e-4) || (w.flags & NOC_WS_ONE_STAGE))) phase = NOC_PHASE_DONE;
-        break;
-      }
+      if (capped) break;
     }
     if (capped || !(bp > 1e-4)) break;                          // P:243-245
     if (w.flags & NOC_WS_ONE_STAGE) break;                      // newton_oc: one stage
   }
-  if constexpr (XLDS) {  // states and controls back to the workspace
+  if constexpr (XLDS) {  // states and controls back to the workspace (every copy is the same)
     wave_fence();
-    for (int i = l; i < (N + 1) * NX; i += 64) Xg[i] = X[i];
-    for (int i = l; i < N * NU; i += 64) Ug[i] = U[i];
+    if (wv == 0) {
+      for (int i = l; i < (N + 1) * NX; i += 64) Xg[i] = X[i];
+      for (int i = l; i < N * NU; i += 64) Ug[i] = U[i];
+    }
   }
-  if (l == 0) {
+  if (lead) {
     w.bp[b] = bp;
     w.rp[b] = rp;
     w.rinc[b] = rinc;
@@ -664,6 +754,39 @@ static hipError_t launch_solve(const noc_family& p, const noc_ipm_ws& w, int mod
   else
     hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, WPS, RESUME, XLDS, true>), dim3(grid), dim3(64),
                        lds, s, p, w, mode, terminal, bp0, max_solves);
+  return hipGetLastError();
+}
+
+// Speculative retries (SPEC waves per trajectory, the one-wave-per-SIMD register budget): when
+// the batch leaves SIMDs idle, a trajectory's workgroup runs SPEC waves on SPEC SIMDs, wave k
+// solving the KKT system and the trial of the k-th candidate of the regularisation's failure chain
+// (rp, rp r_inc, rp r_inc 2 r_inc, ...; P:167-173) at the same point; the accept tests are then
+// replayed in solve order (ipm_solve_kernel), so counters and iterates are the one-wave solver's
+// bit for bit.  A rejected trial no longer costs a KKT solve on the trajectory's serial chain:
+// the heaviest of 512 cart-poles, 492 computed solves, takes 345 rounds at two candidates, 266 at
+// four (tools/spec_estimate.py).  Needs x, u in LDS per wave and no resume.
+// NOC_PERSIST_SPEC=1|2|4 overrides the choice.
+template <int KIND, int NX, int NU>
+static size_t spec_lds_bytes(int N, int spec) {
+  return (size_t)(xlds_off<NX, NU>(N, spec, 0) + spec * xlds_doubles<NX, NU>(N)) * sizeof(double);
+}
+template <int KIND, int NX, int NU>
+static int spec_count(const noc_ipm_ws& w, int simds) {
+  if (w.flags & NOC_WS_RESUME) return 1;
+  const char* env = getenv("NOC_PERSIST_SPEC");  // per launch (A/B sweeps in one process)
+  const char* senv = getenv("NOC_PERSIST_STRUCT");
+  if (senv && atoi(senv) == 0) return 1;
+  int want = env ? atoi(env) : 1;
+  if (want != 2 && want != 4) return 1;
+  if (!env && (simds <= 0 || (long long)w.Bt * want > simds)) return 1;
+  return spec_lds_bytes<KIND, NX, NU>(w.N, want) <= (size_t)want * 40960u ? want : 1;
+}
+template <int KIND, int NX, int NU, int SPEC>
+static hipError_t launch_spec(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
+                              double bp0, int max_solves, hipStream_t s) {
+  const size_t lds = spec_lds_bytes<KIND, NX, NU>(w.N, SPEC);
+  hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 1, false, true, true, SPEC>), dim3(w.Bt), dim3(64 * SPEC),
+                     lds, s, p, w, mode, terminal, bp0, max_solves);
   return hipGetLastError();
 }
 
@@ -733,7 +856,12 @@ static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, in
     static const int simds = device_simds();
     static const char* env = getenv("NOC_PERSIST_WAVES");
     const bool one = env ? atoi(env) == 1 : (simds > 0 && w.Bt <= simds);
-    if (one) return solve_w<KIND, NX, NU, 1>(p, w, mode, terminal, bp0, max_solves, lds, s);
+    if (one) {
+      const int spec = w.order ? 1 : spec_count<KIND, NX, NU>(w, simds);
+      if (spec == 2) return launch_spec<KIND, NX, NU, 2>(p, w, mode, terminal, bp0, max_solves, s);
+      if (spec == 4) return launch_spec<KIND, NX, NU, 4>(p, w, mode, terminal, bp0, max_solves, s);
+      return solve_w<KIND, NX, NU, 1>(p, w, mode, terminal, bp0, max_solves, lds, s);
+    }
     const int heavy = env ? 0 : heavy_count(w, simds);
     if (heavy > 0) return solve_split<KIND, NX, NU>(p, w, mode, terminal, bp0, max_solves, lds, s, heavy);
   }

@@ -143,9 +143,9 @@ NOC_DEV void load_stage(const KKTArgs& a, int traj, size_t si, int j, int l, int
       gload<NX * NX>(a.A + si * (NX * NX), st.A.v);
       gload<NX * NU>(a.Bm + si * (NX * NU), st.B.v);
     }
-    if constexpr (WQ) gload_sym<NX>(a.Q + si * (NX * NX), st.Q);
+    if constexpr (WQ) gload_sym<NX, true>(a.Q + si * (NX * NX), st.Q);
     if constexpr (REST) {
-      gload_sym<NU>(a.R + si * (NU * NU), st.R);
+      gload_sym<NU, true>(a.R + si * (NU * NU), st.R);
       gload<NX * NU>(a.M + si * (NX * NU), st.M.v);
       gload<NU>(a.r + si * NU, st.r.v);
       if constexpr (AFF) {
@@ -615,8 +615,11 @@ struct ArgsSrc {
 // LDS per wave): A, B of chunk slots j < a.ab_slots stay in LDS from phase 1 to phases 3 and 4
 // (lds_ab); a.ab_slots = 0 turns it off at run time.  Not in the two-wave segments (L = 128): their
 // re-reads are L2 hits already, and the slots measured +2.5 % there (profiles/r05/ab_slots/).
+// IO0: reg, pred and feasible are one slot each (a.reg[0], a.pred[0], a.feasible[0]) instead of
+// per-trajectory arrays -- the persistent solver's speculative candidates (ipm_persistent.hip: SPEC)
+// each solve the same blocks with their own regularisation and keep those three in LDS.
 template <int NX, int NU, int L, bool AFF, bool TILED, class SRC, int CACHE = 0, bool HANDOFF = true,
-          bool BIG = false, bool NT3 = false, bool AB = (BIG && ab_supported<NX, NU>())>
+          bool BIG = false, bool NT3 = false, bool AB = (BIG && ab_supported<NX, NU>()), bool IO0 = false>
 NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, const SRC& src) {
   constexpr int KD = kd_width<NX, NU>();
   using ST = typename SRC::Struct;  // structural zeros of A, B (DenseBlocks: none)
@@ -627,7 +630,8 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
   const int len = base + (l < rem ? 1 : 0);
   const int start = l * base + (l < rem ? l : rem);
   const bool last = (l == L - 1);
-  const double reg = a.reg ? a.reg[traj] : 0.0;
+  const int io = IO0 ? 0 : traj;
+  const double reg = a.reg ? a.reg[io] : 0.0;
   const size_t tN = (size_t)traj * N;
   const int cmax = base + (rem ? 1 : 0);
   // LW lanes of one wave in the segment, W waves per segment (W = 2: L = 128, the horizon split
@@ -681,7 +685,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
     if (last) {  // terminal cost (0, 0, 0, p, P)
       set_zero(e.A);
       set_zero(e.nu);
-      gload_sym<NX>(a.P + (size_t)traj * NX * NX, e.J);
+      gload_sym<NX, true>(a.P + (size_t)traj * NX * NX, e.J);
       if constexpr (AFF) { if (a.p) gload<NX>(a.p + (size_t)traj * NX, e.nu.v); }
     } else {
       set_identity(e.A);
@@ -730,7 +734,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       }
     }
     if (a.ablate & 4) {  // phase 1 (+2) only: keep the element alive, skip the rest
-      if (a.pred) a.pred[traj] = e.J(0, 0) + e.A(0, 0) + e.C(0, 0) + e.nu[0] + e.b[0];
+      if (a.pred) a.pred[io] = e.J(0, 0) + e.A(0, 0) + e.C(0, 0) + e.nu[0] + e.b[0];
       return;
     }
     NOC_STAMP(2); NOC_ISA_MARK("phase", 2);
@@ -746,7 +750,7 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       }
     }
     if (last) {  // boundary of the last chunk: the terminal cost itself (reloaded, not kept live)
-      gload_sym<NX>(a.P + (size_t)traj * NX * NX, S);
+      gload_sym<NX, true>(a.P + (size_t)traj * NX * NX, S);
       set_zero(v);
       if constexpr (AFF) { if (a.p) gload<NX>(a.p + (size_t)traj * NX, v.v); }
       if (a.S) gstore_sym<NX>(a.S + (tN + traj + N) * (NX * NX), S);
@@ -933,8 +937,8 @@ NOC_DEV void kkt_scan_wave_src(const KKTArgs& a, const int traj, const int l, co
       }
     }
     if (l == 0) {
-      if (a.pred) a.pred[traj] = pred;
-      if (a.feasible) a.feasible[traj] = feas;
+      if (a.pred) a.pred[io] = pred;
+      if (a.feasible) a.feasible[io] = feas;
     }
     NOC_STAMP(3); NOC_ISA_MARK("phase", 3);
     if (a.mode == MODE_BWD || (a.ablate & 2)) return;

@@ -90,19 +90,24 @@ NOC_DEV double opaque(double v) {
   return v;
 }
 
-// load a full row-major N x N matrix and symmetrise it into packed storage.  The off-diagonal
-// 0.5 (a + b) is opaque: a symmetrised Q(i, j) starts the Riccati sums S = Q + A'SA + ..., and
-// two inlined copies of that step fused it differently -- fma(0.5, a + b, A * SA) in one,
-// 0.5 (a + b) rounded then fma(A, SA, .) in the other (round 6 ISA: six v_fmac_f64 with 0.5 in
-// the A, B-slot path's phase 3, six v_mul_f64 by 0.5 in the re-read path's), so the natural
-// layout's results depended on which path the batch size selected (tests/test_kkt_gpu.py:
-// test_ab_slots_equal_rereads).  Now both round the symmetrised entry first.
-template <int N>
+// load a full row-major N x N matrix and symmetrise it into packed storage.  OPAQUE: the
+// off-diagonal 0.5 (a + b) passes through an empty asm, so it is rounded on its own.  A
+// symmetrised Q(i, j) starts the KKT scan's Riccati sums S = Q + A'SA + ..., and two inlined
+// copies of that step fused it differently -- fma(0.5, a + b, A * SA) in one, 0.5 (a + b) rounded
+// then fma(A, SA, .) in the other (round 6 ISA: six v_fmac_f64 with 0.5 in the A, B-slot path's
+// phase 3, six v_mul_f64 by 0.5 in the re-read path's), so the natural layout's results depended
+// on which path the batch size selected (tests/test_kkt_gpu.py: test_ab_slots_equal_rereads).
+// The scan loads with OPAQUE; the group solves do not (with it in their load of P, c4 measured
+// 5.23 against 4.90 ms on one box, profiles/r06/m/).
+template <int N, bool OPAQUE = false>
 NOC_DEV void gload_sym(const double* __restrict__ src, Sym<N>& S) {
   double t[N * N];
   gload<N * N>(src, t);
   NOC_UNROLL for (int i = 0; i < N; ++i)
-    NOC_UNROLL for (int j = i; j < N; ++j) S(i, j) = (i == j) ? t[i * N + i] : opaque(0.5 * (t[i * N + j] + t[j * N + i]));
+    NOC_UNROLL for (int j = i; j < N; ++j) {
+      const double h = 0.5 * (t[i * N + j] + t[j * N + i]);
+      S(i, j) = (i == j) ? t[i * N + i] : (OPAQUE ? opaque(h) : h);
+    }
 }
 template <int N>
 NOC_DEV void gstore_sym(double* __restrict__ dst, const Sym<N>& S) {

@@ -456,6 +456,45 @@ def test_heavy_first_split_gives_identical_results(heavy, monkeypatch):
         assert np.array_equal(res["0"][k], res[heavy][k]), k
 
 
+@pytest.mark.parametrize("spec", ["2", "4"])
+@pytest.mark.parametrize("N,Bt,mode,seed", [(200, 512, "par", 11), (60, 40, "seq", 3), (200, 24, "par", 5)])
+def test_speculative_candidates_equal_one_wave(spec, N, Bt, mode, seed, monkeypatch):
+    """Speculative retries (ipm_persistent.hip: SPEC waves per trajectory, wave k solving the
+    k-th candidate of the regularisation's failure chain, the accept tests replayed in solve
+    order) against the one-wave solver: controls, states and every counter bit-identical, for a
+    whole solve and for one capped at a solve count that falls inside a round of candidates and
+    then resumed (on the one-wave resume instance).  The first case is the c3 8-GPU slice size
+    (512 cart-poles, N = 200), with accounted repeats at the rp clip."""
+    monkeypatch.setenv("NOC_PERSIST_WIDE", "0")
+    from noc import _lib
+    from noc.ipm import BatchedIPM
+    ocp, x0, u0 = _resume_case("cartpole", N, Bt, seed=seed)
+    m = _lib.MODE_PAR if mode == "par" else _lib.MODE_SEQ
+    keys = ("u", "x", "kkt_solves", "total_it", "phase", "bp", "rp", "rinc", "repeats", "cost",
+            "inner", "it", "hu", "gnorm")
+
+    def run(s, cap=None):
+        monkeypatch.setenv("NOC_PERSIST_SPEC", s)
+        eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
+        eng.load(u0, x0)
+        if cap is None:
+            eng.solve_persistent(mode=m, schedule="index")
+        else:
+            eng.solve_persistent(mode=m, schedule="index", max_solves=cap)
+            eng.solve_persistent(mode=m, schedule="index", resume=True)
+        torch.cuda.synchronize()
+        return {k: eng.t[k].cpu().numpy().copy() for k in keys}
+
+    ref = run("1")
+    assert np.all(ref["phase"] == _lib.PHASE_DONE)
+    for cap in (None, 37):
+        got = run(spec, cap)
+        for k in keys:
+            assert np.array_equal(ref[k], got[k]), (k, cap)
+    if N == 200 and Bt == 512:
+        assert int(ref["repeats"].sum()) > 0  # the rp-clip accounting is exercised
+
+
 def test_rp_update_rounds_like_the_reference():
     """The regularisation update after an accepted step, rp * max(1/3, 1 - (2 gain - 1) ** 3)
     (P:167-173, S:139-143), rounds like the reference: the cube as lax.integer_pow, c * (c * c),
