@@ -766,20 +766,35 @@ static hipError_t launch_solve(const noc_family& p, const noc_ipm_ws& w, int mod
 // the heaviest of 512 cart-poles, 492 computed solves, takes 345 rounds at two candidates, 266 at
 // four (tools/spec_estimate.py).  Needs x, u in LDS per wave and no resume.
 // NOC_PERSIST_SPEC=1|2|4 overrides the choice.
+static size_t spec_lds_rt(int nx, int nu, int N, int spec) {  // = xlds_off(N, spec, 0) + spec x, u
+  const long long slots = ((long long)N * nu * (nx + 1) + nx + 1) & ~1LL;
+  const long long xu = ((long long)(N + 1) * nx + (long long)N * nu + 1) & ~1LL;
+  return (size_t)(spec * (slots + state_doubles() + xu) + specio_doubles(spec)) * sizeof(double);
+}
 template <int KIND, int NX, int NU>
 static size_t spec_lds_bytes(int N, int spec) {
   return (size_t)(xlds_off<NX, NU>(N, spec, 0) + spec * xlds_doubles<NX, NU>(N)) * sizeof(double);
 }
-template <int KIND, int NX, int NU>
-static int spec_count(const noc_ipm_ws& w, int simds) {
-  if (w.flags & NOC_WS_RESUME) return 1;
-  const char* env = getenv("NOC_PERSIST_SPEC");  // per launch (A/B sweeps in one process)
+// Candidates per trajectory for this launch: 4 when four waves per trajectory still leave a SIMD
+// each (B <= #SIMDs / 4), else 2 (B <= #SIMDs / 2), else 1; 1 for a resume or an ordered launch
+// (their trajectories started elsewhere), and when x, u of every wave do not fit 40 KB of LDS per
+// wave.  The families with a one-wave instance only (cart-pole).  NOC_PERSIST_SPEC=1|2|4 forces it.
+static int spec_auto(const noc_family& p, const noc_ipm_ws& w, int simds, bool launch_state) {
+  if (p.kind != NOC_FAMILY_CARTPOLE) return 1;
+  if (launch_state && ((w.flags & NOC_WS_RESUME) || w.order)) return 1;
   const char* senv = getenv("NOC_PERSIST_STRUCT");
   if (senv && atoi(senv) == 0) return 1;
-  int want = env ? atoi(env) : 1;
+  const char* env = getenv("NOC_PERSIST_SPEC");  // per launch (A/B sweeps in one process)
+  int want;
+  if (env) {
+    want = atoi(env);
+  } else if (simds <= 0) {
+    want = 1;
+  } else {
+    want = (long long)w.Bt * 4 <= simds ? 4 : ((long long)w.Bt * 2 <= simds ? 2 : 1);
+  }
   if (want != 2 && want != 4) return 1;
-  if (!env && (simds <= 0 || (long long)w.Bt * want > simds)) return 1;
-  return spec_lds_bytes<KIND, NX, NU>(w.N, want) <= (size_t)want * 40960u ? want : 1;
+  return spec_lds_rt(p.nx, p.nu, w.N, want) <= (size_t)want * 40960u ? want : 1;
 }
 template <int KIND, int NX, int NU, int SPEC>
 static hipError_t launch_spec(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
@@ -857,7 +872,7 @@ static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, in
     static const char* env = getenv("NOC_PERSIST_WAVES");
     const bool one = env ? atoi(env) == 1 : (simds > 0 && w.Bt <= simds);
     if (one) {
-      const int spec = w.order ? 1 : spec_count<KIND, NX, NU>(w, simds);
+      const int spec = spec_auto(p, w, simds, true);
       if (spec == 2) return launch_spec<KIND, NX, NU, 2>(p, w, mode, terminal, bp0, max_solves, s);
       if (spec == 4) return launch_spec<KIND, NX, NU, 4>(p, w, mode, terminal, bp0, max_solves, s);
       return solve_w<KIND, NX, NU, 1>(p, w, mode, terminal, bp0, max_solves, lds, s);
@@ -937,12 +952,20 @@ static hipError_t solve_family(const noc_family& p, const noc_ipm_ws& w, int mod
 // 35.2 us -- profiles/r02/wide/crossover.jsonl).  NOC_PERSIST_WIDE=0|1 overrides.
 // (Re-packing the last <= #CUs trajectories of a large batch onto it was measured and dropped:
 // those are Newton retries, KKT-bound, and the wide KKT solve is no faster -- DESIGN.md §3.7.)
+// Where the speculative candidates apply (cart-pole, B <= #SIMDs / 2) and the horizon gives the
+// one-wave kernel at most five stages per lane (N <= 320), they beat the wide kernel: cart-pole
+// B = 1 N = 200 / 300 5.19 / 5.92 ms against 5.88 / 6.32 ms, N = 200 B = 64 / 256 7.54 / 8.30 ms
+// against 9.53 / 10.28 ms; at N = 400 the wide kernel is ahead (6.57 vs 7.02 ms;
+// profiles/r06/n/).  The choice ignores resume and order, so a capped solve resumes on the kernel
+// family (one-wave) it started on.
 static bool use_wide(const noc_family& p, const noc_ipm_ws& w) {
   const char* env = getenv("NOC_PERSIST_WIDE");
   if (env && atoi(env) == 0) return false;
   if (!ipm_wide_supported(p, w.N)) return false;
   if (env && atoi(env) == 1) return true;
-  static const int cus = device_simds() / 4;
+  static const int simds = device_simds();
+  const int cus = simds / 4;
+  if (w.N <= 320 && spec_auto(p, w, simds, false) > 1) return false;
   return cus > 0 && w.Bt <= cus && w.N > 128;
 }
 

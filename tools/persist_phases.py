@@ -16,6 +16,7 @@ subs = {6: "trial_costs", 7: "costate_scan", 9: "kkt_elements", 10: "kkt_cross_l
 # one-wave kernel throughout (B = 1 would run the wide kernel); both block layouts (round 6:
 # NOC_PERSIST_STRUCT=1 structure-aware compact blocks, 0 dense)
 os.environ["NOC_PERSIST_WIDE"] = "0"
+os.environ["NOC_PERSIST_SPEC"] = "1"  # one wave per trajectory (no speculative candidates)
 CONFIGS = [("pendulum", 50, 1), ("cartpole", 200, 1), ("cartpole", 200, 512), ("cartpole", 200, 4096)]
 for name, N, B, struct in [c + (s,) for c in CONFIGS for s in ("1", "0")]:
     os.environ["NOC_PERSIST_STRUCT"] = struct

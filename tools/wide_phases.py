@@ -23,6 +23,7 @@ for name, N, B in CONFIGS:
             continue
         os.environ["NOC_PERSIST_WIDE"] = wide
         os.environ["NOC_WIDE_WAVES"] = "2" if waves == "-" else waves
+        os.environ["NOC_PERSIST_SPEC"] = "1"
         ocp = problems.make_problem(name, N)
         x0, u0 = problems.initial_conditions(name, N, B, seed=11)
         eng = BatchedIPM(ocp.family, N, B, persistent=True)
