@@ -155,12 +155,12 @@ struct CompactSrc {
 // instance, which computes the same doubles).
 // SPEC: waves per trajectory, each solving one candidate of the regularisation's failure chain
 // (speculative retries, below); 1 = the plain solver.  SPEC > 1 needs XLDS (every wave keeps its
-// own copy of x, u) and runs no RESUME launch.
+// own copy of x, u).
 template <int KIND, int NX, int NU, int WPS, bool RESUME, bool XLDS, bool STRUCT, int SPEC = 1>
 __global__ __launch_bounds__(64 * SPEC, WPS) void ipm_solve_kernel(noc_family prm, noc_ipm_ws w, int mode,
                                                                 int terminal, double bp0,
                                                                 int max_solves) {
-  static_assert(SPEC == 1 || (XLDS && !RESUME), "speculative waves keep x, u in LDS, no resume");
+  static_assert(SPEC == 1 || XLDS, "speculative waves keep x, u in LDS");
   // one wave (= one 64-thread workgroup) per trajectory -- SPEC waves with SPEC > 1; w.order: the
   // launch order (a permutation)
   const int b = w.order ? w.order[blockIdx.x] : (int)blockIdx.x;
@@ -275,6 +275,7 @@ __global__ __launch_bounds__(64 * SPEC, WPS) void ipm_solve_kernel(noc_family pr
     if constexpr (RESUME) entry = NOC_PHASE_ROLLOUT;
     bool stage_done = false;
     while (!stage_done) {  // ---------------- Newton iterations (P:127-225) ----------------
+      const bool relinearized = relinearize;  // uniform over the workgroup
       if (relinearize) {
         // linearise the own chunk (P:13-28): A = fx, B = fu, cx, cu, stage cost
         struct LinOut {
@@ -526,8 +527,10 @@ __global__ __launch_bounds__(64 * SPEC, WPS) void ipm_solve_kernel(noc_family pr
       NOC_PHASE(2);
       wave_fence();  // the terminal Hessian (stage-0 lane) and the blocks before the scan
       // SPEC > 1: every wave has written the blocks (the same doubles) and read w.lc before any
-      // wave's trial overwrites w.lc
-      if constexpr (SPEC > 1) __syncthreads();
+      // wave's trial overwrites w.lc (a retry reads neither: no barrier)
+      if constexpr (SPEC > 1) {
+        if (relinearized) __syncthreads();
+      }
       {  // park the state (every lane stores the same values)
         IpmState* st = state_slot<NX, NU>(N, SPEC, wv);
         st->bp = bp; st->rp = rp; st->rinc = rinc; st->cost = cost; st->hu = hu; st->gnorm = gnorm;
@@ -764,7 +767,7 @@ static hipError_t launch_solve(const noc_family& p, const noc_ipm_ws& w, int mod
 // replayed in solve order (ipm_solve_kernel), so counters and iterates are the one-wave solver's
 // bit for bit.  A rejected trial no longer costs a KKT solve on the trajectory's serial chain:
 // the heaviest of 512 cart-poles, 492 computed solves, takes 345 rounds at two candidates, 266 at
-// four (tools/spec_estimate.py).  Needs x, u in LDS per wave and no resume.
+// four (tools/spec_estimate.py).  Needs x, u in LDS per wave.
 // NOC_PERSIST_SPEC=1|2|4 overrides the choice.
 static size_t spec_lds_rt(int nx, int nu, int N, int spec) {  // = xlds_off(N, spec, 0) + spec x, u
   const long long slots = ((long long)N * nu * (nx + 1) + nx + 1) & ~1LL;
@@ -776,12 +779,13 @@ static size_t spec_lds_bytes(int N, int spec) {
   return (size_t)(xlds_off<NX, NU>(N, spec, 0) + spec * xlds_doubles<NX, NU>(N)) * sizeof(double);
 }
 // Candidates per trajectory for this launch: 4 when four waves per trajectory still leave a SIMD
-// each (B <= #SIMDs / 4), else 2 (B <= #SIMDs / 2), else 1; 1 for a resume or an ordered launch
-// (their trajectories started elsewhere), and when x, u of every wave do not fit 40 KB of LDS per
-// wave.  The families with a one-wave instance only (cart-pole).  NOC_PERSIST_SPEC=1|2|4 forces it.
+// each (B <= #SIMDs / 4), else 2 (B <= #SIMDs / 2), else 1; 1 for an ordered launch (its grid is
+// the whole batch, most of it done), and when x, u of every wave do not fit 40 KB of LDS per wave.
+// A resume may run them (the tail of a large batch, gathered: BatchedIPM.solve_persistent).  The
+// families with a one-wave instance only (cart-pole).  NOC_PERSIST_SPEC=1|2|4 forces it.
 static int spec_auto(const noc_family& p, const noc_ipm_ws& w, int simds, bool launch_state) {
   if (p.kind != NOC_FAMILY_CARTPOLE) return 1;
-  if (launch_state && ((w.flags & NOC_WS_RESUME) || w.order)) return 1;
+  if (launch_state && w.order) return 1;
   const char* senv = getenv("NOC_PERSIST_STRUCT");
   if (senv && atoi(senv) == 0) return 1;
   const char* env = getenv("NOC_PERSIST_SPEC");  // per launch (A/B sweeps in one process)
@@ -796,12 +800,18 @@ static int spec_auto(const noc_family& p, const noc_ipm_ws& w, int simds, bool l
   if (want != 2 && want != 4) return 1;
   return spec_lds_rt(p.nx, p.nu, w.N, want) <= (size_t)want * 40960u ? want : 1;
 }
+// grid: workgroups = the entries of w.order this launch solves (w.Bt without an order)
 template <int KIND, int NX, int NU, int SPEC>
 static hipError_t launch_spec(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
-                              double bp0, int max_solves, hipStream_t s) {
+                              double bp0, int max_solves, hipStream_t s, int grid = -1) {
+  if (grid < 0) grid = w.Bt;
   const size_t lds = spec_lds_bytes<KIND, NX, NU>(w.N, SPEC);
-  hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 1, false, true, true, SPEC>), dim3(w.Bt), dim3(64 * SPEC),
-                     lds, s, p, w, mode, terminal, bp0, max_solves);
+  if (w.flags & NOC_WS_RESUME)
+    hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 1, true, true, true, SPEC>), dim3(grid), dim3(64 * SPEC),
+                       lds, s, p, w, mode, terminal, bp0, max_solves);
+  else
+    hipLaunchKernelGGL((ipm_solve_kernel<KIND, NX, NU, 1, false, true, true, SPEC>), dim3(grid), dim3(64 * SPEC),
+                       lds, s, p, w, mode, terminal, bp0, max_solves);
   return hipGetLastError();
 }
 
@@ -850,9 +860,14 @@ static hipError_t solve_split(const noc_family& p, const noc_ipm_ws& w, int mode
   hipError_t e;
   if ((e = hipEventRecord(fork, s)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(s2, fork, 0)) != hipSuccess) return e;
-  // the heavy launch first, so its workgroups are placed before the two-wave ones fill the SIMDs
-  if ((e = solve_w<KIND, NX, NU, 1>(p, w, mode, terminal, bp0, max_solves, lds, s, heavy)) != hipSuccess)
-    return e;
+  // the heavy launch first, so its workgroups are placed before the two-wave ones fill the SIMDs;
+  // NOC_PERSIST_HEAVY_SPEC=2: the heavy trajectories with two speculative candidates each
+  const char* hs = getenv("NOC_PERSIST_HEAVY_SPEC");
+  if (hs && atoi(hs) == 2 && spec_lds_bytes<KIND, NX, NU>(w.N, 2) <= 2 * 40960u)
+    e = launch_spec<KIND, NX, NU, 2>(p, w, mode, terminal, bp0, max_solves, s, heavy);
+  else
+    e = solve_w<KIND, NX, NU, 1>(p, w, mode, terminal, bp0, max_solves, lds, s, heavy);
+  if (e != hipSuccess) return e;
   noc_ipm_ws rest = w;
   rest.order = w.order + heavy;
   if ((e = solve_w<KIND, NX, NU, 2>(p, rest, mode, terminal, bp0, max_solves, lds, s2, w.Bt - heavy)) !=

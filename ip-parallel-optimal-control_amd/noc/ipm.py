@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import math
 import ctypes
+import os
 from typing import Optional
 
 import numpy as np
@@ -194,8 +195,10 @@ class BatchedIPM:
         terminal = default_terminal(mode) if terminal is None else terminal
         if schedule not in ("auto", "cost", "index", "probe"):
             raise ValueError(schedule)
-        if schedule == "auto":
+        auto = schedule == "auto"
+        if auto:
             schedule = "probe" if (not resume and self.Bt > self._resident_slots()) else "index"
+        tail = auto and self._tail_eligible()
         if schedule == "probe" and not resume:
             k = min(int(self.PROBE_SOLVES), int(max_solves))
             self._launch(mode, terminal, bp0, k, resume=False, order=None)
@@ -208,8 +211,71 @@ class BatchedIPM:
             return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
         ordered = not resume and schedule == "cost"
         self._order = self.launch_order(mode, terminal, bp0) if ordered else None
-        self._launch(mode, terminal, bp0, max_solves, resume=resume, order=self._order)
+        if tail and not ordered:
+            self._tail_ladder(mode, terminal, bp0, max_solves, resume, None, 0)
+        else:
+            self._launch(mode, terminal, bp0, max_solves, resume=resume, order=self._order)
         return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
+
+    # The tail of a batch at one wave per SIMD (cart-pole, #SIMDs / 2 < B <= #SIMDs: the 4-GPU
+    # slice of c3): the launch is capped at solve counts TAIL_CAPS, and once the trajectories
+    # still running fit two waves each on the SIMDs, they are gathered into a small workspace and
+    # resumed there -- where the solver runs speculative candidates (two or four waves per
+    # trajectory, csrc/ipm_persistent.hip: SPEC), so the stragglers' serial chains of rejected
+    # trials shorten.  Results, counters and iterates are the uninterrupted solve's bit for bit
+    # (capped-and-resumed solves and the candidates both are).  Measured (profiles/r06/o/): 1024
+    # cart-poles 13.83-13.91 -> 13.30-13.34 ms with the caps below (cap 256: 205 still running,
+    # resumed with four candidates); not at 2 waves per SIMD (2048: equal) nor after the probe
+    # launch (4096: 29-31 vs 25 ms -- it breaks the cost-ordered resume), so not there.
+    # NOC_PERSIST_TAIL=0 turns it off; NOC_PERSIST_TAIL_CAPS="a,b,..." sets the caps.
+    TAIL_CAPS = (256, 384, 512)
+    _SHARED_FIELDS = ("x", "u", "x0") + tuple(_lib.WS_STATE_FIELDS) + tuple(_lib.WS_INT_FIELDS)
+
+    def _simds(self) -> int:
+        return 4 * torch.cuda.get_device_properties(self.device).multi_processor_count
+
+    def _tail_eligible(self) -> bool:
+        if os.environ.get("NOC_PERSIST_TAIL", "1") == "0" or os.environ.get("NOC_PERSIST_SPEC") == "1":
+            return False
+        if os.environ.get("NOC_PERSIST_STRUCT") == "0":
+            return False
+        simds = self._simds()
+        return (self.persistent and self.family.kind == _lib.FAMILY_CARTPOLE and self.N <= 320
+                and simds < 2 * self.Bt <= 2 * simds)
+
+    def _tail_caps(self):
+        env = os.environ.get("NOC_PERSIST_TAIL_CAPS")
+        return tuple(int(c) for c in env.split(",")) if env else self.TAIL_CAPS
+
+    def _tail_ladder(self, mode, terminal, bp0, max_solves, resume, order, done_cap):
+        simds = self._simds()
+        self.tail_log = []
+        for cap in self._tail_caps():
+            if cap <= done_cap:
+                continue
+            if cap >= max_solves:
+                break
+            self._launch(mode, terminal, bp0, cap, resume=resume, order=order)
+            resume = True
+            run = torch.nonzero(self.t["phase"] != _lib.PHASE_DONE).flatten()
+            R = int(run.numel())
+            self.tail_log.append((cap, R))
+            if R == 0:
+                return
+            if 2 * R <= simds:
+                self._tail_gather(run, mode, terminal, bp0, max_solves)
+                return
+        self._launch(mode, terminal, bp0, max_solves, resume=resume, order=order)
+
+    def _tail_gather(self, run, mode, terminal, bp0, max_solves):
+        sub = BatchedIPM(self.family, self.N, int(run.numel()), device=self.device, lanes=64,
+                         persistent=True)
+        for k in self._SHARED_FIELDS:
+            sub.t[k].copy_(self.t[k].index_select(0, run))
+        sub.ws.flags = self.ws.flags
+        sub._launch(mode, terminal, bp0, max_solves, resume=True, order=None)
+        for k in self._SHARED_FIELDS:
+            self.t[k].index_copy_(0, run, sub.t[k])
 
     def _launch(self, mode, terminal, bp0, max_solves, resume, order):
         """one noc_ipm_solve (resume: NOC_WS_RESUME; order: ws.order, a permutation or None)"""

@@ -432,8 +432,8 @@ def test_wide_solve_matches_one_wave_kernel(name, N, Bt, mode, waves, monkeypatc
         assert np.max(np.abs(Uw[b] - Un[b])) <= 1e-6 * max(1.0, float(np.max(np.abs(Un))))
 
 
-@pytest.mark.parametrize("heavy", ["1", "64"])
-def test_heavy_first_split_gives_identical_results(heavy, monkeypatch):
+@pytest.mark.parametrize("heavy,hspec", [("1", "0"), ("64", "0"), ("64", "2")])
+def test_heavy_first_split_gives_identical_results(heavy, hspec, monkeypatch):
     """The probe-ordered resume of a batch larger than one wave per SIMD with its first `heavy`
     launch-order entries on the one-wave instance and the rest on the two-wave instance,
     concurrently on two streams (NOC_PERSIST_HEAVY, ipm_persistent.hip: solve_split): every
@@ -445,6 +445,7 @@ def test_heavy_first_split_gives_identical_results(heavy, monkeypatch):
     ocp, x0, u0 = _resume_case("cartpole", N, Bt, seed=6)
     keys = ("u", "x", "kkt_solves", "total_it", "phase", "bp", "rp", "rinc", "repeats")
     res = {}
+    monkeypatch.setenv("NOC_PERSIST_HEAVY_SPEC", hspec)  # 2: the heavy launch speculates
     for h in ("0", heavy):
         monkeypatch.setenv("NOC_PERSIST_HEAVY", h)
         eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
@@ -463,7 +464,7 @@ def test_speculative_candidates_equal_one_wave(spec, N, Bt, mode, seed, monkeypa
     k-th candidate of the regularisation's failure chain, the accept tests replayed in solve
     order) against the one-wave solver: controls, states and every counter bit-identical, for a
     whole solve and for one capped at a solve count that falls inside a round of candidates and
-    then resumed (on the one-wave resume instance).  The first case is the c3 8-GPU slice size
+    then resumed (on the speculative resume instance).  The first case is the c3 8-GPU slice size
     (512 cart-poles, N = 200), with accounted repeats at the rp clip."""
     monkeypatch.setenv("NOC_PERSIST_WIDE", "0")
     from noc import _lib
@@ -493,6 +494,40 @@ def test_speculative_candidates_equal_one_wave(spec, N, Bt, mode, seed, monkeypa
             assert np.array_equal(ref[k], got[k]), (k, cap)
     if N == 200 and Bt == 512:
         assert int(ref["repeats"].sum()) > 0  # the rp-clip accounting is exercised
+
+
+@pytest.mark.parametrize("extra,caps", [("half", "20,40,60,90,130,180,250,350,500"),
+                                        ("full", "20,40,60,90,130,180,250,350,500")])
+def test_tail_schedule_equals_plain_launch(extra, caps, monkeypatch):
+    """BatchedIPM.solve_persistent's tail schedule (launches capped at NOC_PERSIST_TAIL_CAPS, then
+    the trajectories still running gathered into a small workspace and resumed with speculative
+    candidates) against the plain schedule: controls, states and counters bit-identical.  Batches
+    just beyond half the SIMDs and at one wave per SIMD exactly (the c3 4-GPU slice's shape)."""
+    monkeypatch.setenv("NOC_PERSIST_WIDE", "0")
+    from noc.ipm import BatchedIPM
+    simds = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    N = 60
+    Bt = simds // 2 + 77 if extra == "half" else simds
+    ocp, x0, u0 = _resume_case("cartpole", N, Bt, seed=9)
+    # (not "repeats": the count of retries accounted without recomputation depends on where the
+    # caps fall -- a resume inside a run of identical retries at the rp clip computes its first
+    # solve -- while the solve counts, states and controls do not)
+    keys = ("u", "x", "kkt_solves", "total_it", "phase", "bp", "rp", "rinc", "cost", "inner", "it",
+            "hu", "gnorm")
+    res, logs = {}, {}
+    for tail in ("0", "1"):
+        monkeypatch.setenv("NOC_PERSIST_TAIL", tail)
+        monkeypatch.setenv("NOC_PERSIST_TAIL_CAPS", caps)
+        eng = BatchedIPM(ocp.family, N, Bt, lanes=64, persistent=True)
+        eng.load(u0, x0)
+        eng.solve_persistent()
+        torch.cuda.synchronize()
+        res[tail] = {k: eng.t[k].cpu().numpy().copy() for k in keys}
+        logs[tail] = getattr(eng, "tail_log", None)
+    assert logs["1"], "the tail schedule did not run"
+    assert any(2 * r <= simds for _, r in logs["1"]) or logs["1"][-1][1] == 0, logs["1"]
+    for k in keys:
+        assert np.array_equal(res["0"][k], res["1"][k]), k
 
 
 def test_rp_update_rounds_like_the_reference():
