@@ -226,9 +226,13 @@ int noc_ipm_promote(const noc_ipm_ws* ws, void* stream);
  * of every trajectory in ONE launch, one wave64 per trajectory running its own reference control
  * flow back to back (no per-step launches, no host polls, no lockstep across trajectories).
  * Same arithmetic and results as the noc_ipm_init + noc_ipm_step loop at lanes = 64 -- except that
- * a batch of at most one trajectory per CU runs the wide kernel (four waves per trajectory, blocks
- * in LDS; same control flow, the scans associate differently, so iterates agree to fp64 rounding,
- * not bitwise); the environment variable NOC_PERSIST_WIDE=0 forces the one-wave kernel.  Requires
+ * a batch of at most one trajectory per CU with N > 128 runs the wide kernel (four waves per
+ * trajectory, blocks in LDS; same control flow, the scans associate differently, so iterates agree
+ * to fp64 rounding, not bitwise); the environment variable NOC_PERSIST_WIDE=0 forces the one-wave
+ * kernel.  Cart-pole batches of at most half as many trajectories as SIMDs with N <= 320 instead
+ * run two or four waves per trajectory, each solving one candidate regularisation of the retry
+ * chain ahead of the accept test (speculative retries): the one-wave kernel's results bit for bit
+ * (NOC_PERSIST_SPEC=1 forces one wave).  Requires
  * ws->lanes == 64 and a KKT step that fits in LDS (noc_ipm_solve_supported).  A trajectory that
  * reaches max_solves KKT solves stops with phase != NOC_PHASE_DONE.  On return (stream order)
  * u, x, bp, rp, r_inc, cost, hu, it, total_it, kkt_solves and phase hold the final state. */
