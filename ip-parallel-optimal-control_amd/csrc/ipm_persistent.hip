@@ -838,18 +838,38 @@ static hipError_t solve_w(const noc_family& p, const noc_ipm_ws& w, int mode, in
 // BatchedIPM.solve_persistent) -- run on the one-wave instance, a SIMD of their own, concurrently
 // with the rest on the two-wave instance (second stream, event fork / join).  Every trajectory's
 // result is the same on either instance (tested).  NOC_PERSIST_HEAVY=<n> sets the count.
-static int heavy_count(const noc_ipm_ws& w, int simds) {
+// By default (cart-pole, N <= 320, #SIMDs / 2 < B <= 2 #SIMDs: the c3 slices of 2 and 4 GPUs)
+// the costliest #SIMDs / 4 (B <= #SIMDs) or #SIMDs / 8 trajectories of the probe order run two
+// speculative candidates each, the rest on the one- or two-wave instance: 1024 cart-poles
+// 13.8-13.9 -> 11.4-11.6 ms, 2048 17.9 -> 16.3-16.8 ms (probe order alone; profiles/r06/t/).  At
+// c3 (4096) it measured slower (profiles/r06/q/), so not there.  NOC_PERSIST_HEAVY=<n> sets the
+// count, NOC_PERSIST_HEAVY_SPEC=0|2 the candidates (0 turns the default split off).
+static int heavy_count(const noc_ipm_ws& w, int simds, bool* spec2) {
   const char* env = getenv("NOC_PERSIST_HEAVY");  // per launch (A/B sweeps in one process)
-  if (!w.order || simds <= 0 || w.Bt <= simds || !env) return 0;
-  int h = atoi(env);
+  const char* hs = getenv("NOC_PERSIST_HEAVY_SPEC");
+  *spec2 = false;
+  if (!w.order || simds <= 0) return 0;
+  int h;
+  bool sp;
+  if (env) {
+    h = atoi(env);
+    sp = hs && atoi(hs) == 2;
+    if (w.Bt <= (sp ? simds / 2 : simds)) return 0;
+  } else {
+    if ((hs && atoi(hs) == 0) || w.N > 320 || w.Bt <= simds / 2 || w.Bt > 2 * simds) return 0;
+    h = w.Bt <= simds ? simds / 4 : simds / 8;
+    sp = true;
+  }
   if (h < 0) h = 0;
   if (h > simds / 2) h = simds / 2;
+  *spec2 = sp;
   return h < w.Bt ? h : 0;
 }
 
-template <int KIND, int NX, int NU>
+template <int KIND, int NX, int NU, int REST_WPS = 2>
 static hipError_t solve_split(const noc_family& p, const noc_ipm_ws& w, int mode, int terminal,
-                              double bp0, int max_solves, size_t lds, hipStream_t s, int heavy) {
+                              double bp0, int max_solves, size_t lds, hipStream_t s, int heavy,
+                              bool spec2) {
   thread_local hipStream_t s2 = nullptr;
   thread_local hipEvent_t fork = nullptr, join = nullptr;
   if (!s2) {
@@ -861,16 +881,15 @@ static hipError_t solve_split(const noc_family& p, const noc_ipm_ws& w, int mode
   if ((e = hipEventRecord(fork, s)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(s2, fork, 0)) != hipSuccess) return e;
   // the heavy launch first, so its workgroups are placed before the two-wave ones fill the SIMDs;
-  // NOC_PERSIST_HEAVY_SPEC=2: the heavy trajectories with two speculative candidates each
-  const char* hs = getenv("NOC_PERSIST_HEAVY_SPEC");
-  if (hs && atoi(hs) == 2 && spec_lds_bytes<KIND, NX, NU>(w.N, 2) <= 2 * 40960u)
+  // spec2: the heavy trajectories with two speculative candidates each
+  if (spec2 && spec_lds_bytes<KIND, NX, NU>(w.N, 2) <= 2 * 40960u)
     e = launch_spec<KIND, NX, NU, 2>(p, w, mode, terminal, bp0, max_solves, s, heavy);
   else
     e = solve_w<KIND, NX, NU, 1>(p, w, mode, terminal, bp0, max_solves, lds, s, heavy);
   if (e != hipSuccess) return e;
   noc_ipm_ws rest = w;
   rest.order = w.order + heavy;
-  if ((e = solve_w<KIND, NX, NU, 2>(p, rest, mode, terminal, bp0, max_solves, lds, s2, w.Bt - heavy)) !=
+  if ((e = solve_w<KIND, NX, NU, REST_WPS>(p, rest, mode, terminal, bp0, max_solves, lds, s2, w.Bt - heavy)) !=
       hipSuccess)
     return e;
   if ((e = hipEventRecord(join, s2)) != hipSuccess) return e;
@@ -887,13 +906,18 @@ static hipError_t solve_t(const noc_family& p, const noc_ipm_ws& w, int mode, in
     static const char* env = getenv("NOC_PERSIST_WAVES");
     const bool one = env ? atoi(env) == 1 : (simds > 0 && w.Bt <= simds);
     if (one) {
+      bool sp1 = false;
+      const int heavy1 = env ? 0 : heavy_count(w, simds, &sp1);
+      if (heavy1 > 0)
+        return solve_split<KIND, NX, NU, 1>(p, w, mode, terminal, bp0, max_solves, lds, s, heavy1, sp1);
       const int spec = spec_auto(p, w, simds, true);
       if (spec == 2) return launch_spec<KIND, NX, NU, 2>(p, w, mode, terminal, bp0, max_solves, s);
       if (spec == 4) return launch_spec<KIND, NX, NU, 4>(p, w, mode, terminal, bp0, max_solves, s);
       return solve_w<KIND, NX, NU, 1>(p, w, mode, terminal, bp0, max_solves, lds, s);
     }
-    const int heavy = env ? 0 : heavy_count(w, simds);
-    if (heavy > 0) return solve_split<KIND, NX, NU>(p, w, mode, terminal, bp0, max_solves, lds, s, heavy);
+    bool sp = false;
+    const int heavy = env ? 0 : heavy_count(w, simds, &sp);
+    if (heavy > 0) return solve_split<KIND, NX, NU>(p, w, mode, terminal, bp0, max_solves, lds, s, heavy, sp);
   }
   return solve_w<KIND, NX, NU, 2>(p, w, mode, terminal, bp0, max_solves, lds, s);
 }

@@ -432,8 +432,9 @@ def test_wide_solve_matches_one_wave_kernel(name, N, Bt, mode, waves, monkeypatc
         assert np.max(np.abs(Uw[b] - Un[b])) <= 1e-6 * max(1.0, float(np.max(np.abs(Un))))
 
 
-@pytest.mark.parametrize("heavy,hspec", [("1", "0"), ("64", "0"), ("64", "2")])
-def test_heavy_first_split_gives_identical_results(heavy, hspec, monkeypatch):
+@pytest.mark.parametrize("heavy,hspec,beyond", [("1", "0", True), ("64", "0", True), ("64", "2", True),
+                                                ("96", "2", False)])
+def test_heavy_first_split_gives_identical_results(heavy, hspec, beyond, monkeypatch):
     """The probe-ordered resume of a batch larger than one wave per SIMD with its first `heavy`
     launch-order entries on the one-wave instance and the rest on the two-wave instance,
     concurrently on two streams (NOC_PERSIST_HEAVY, ipm_persistent.hip: solve_split): every
@@ -441,7 +442,9 @@ def test_heavy_first_split_gives_identical_results(heavy, hspec, monkeypatch):
     monkeypatch.setenv("NOC_PERSIST_WIDE", "0")
     from noc.ipm import BatchedIPM
     simds = 4 * torch.cuda.get_device_properties(0).multi_processor_count
-    N, Bt = 30, simds + 77   # beyond one wave per SIMD: the two-wave instance, split engaged
+    # beyond one wave per SIMD: the two-wave instance, split engaged; else (hspec = 2 only) at one
+    # wave per SIMD, the rest on the one-wave instance
+    N, Bt = 30, (simds + 77 if beyond else simds - 100)
     ocp, x0, u0 = _resume_case("cartpole", N, Bt, seed=6)
     keys = ("u", "x", "kkt_solves", "total_it", "phase", "bp", "rp", "rinc", "repeats")
     res = {}
