@@ -838,12 +838,13 @@ static hipError_t solve_w(const noc_family& p, const noc_ipm_ws& w, int mode, in
 // BatchedIPM.solve_persistent) -- run on the one-wave instance, a SIMD of their own, concurrently
 // with the rest on the two-wave instance (second stream, event fork / join).  Every trajectory's
 // result is the same on either instance (tested).  NOC_PERSIST_HEAVY=<n> sets the count.
-// By default (cart-pole, N <= 320, #SIMDs / 2 < B <= 2 #SIMDs: the c3 slices of 2 and 4 GPUs)
-// the costliest #SIMDs / 4 (B <= #SIMDs) or #SIMDs / 8 trajectories of the probe order run two
-// speculative candidates each, the rest on the one- or two-wave instance: 1024 cart-poles
-// 13.8-13.9 -> 11.4-11.6 ms, 2048 17.9 -> 16.3-16.8 ms (probe order alone; profiles/r06/t/).  At
-// c3 (4096) it measured slower (profiles/r06/q/), so not there.  NOC_PERSIST_HEAVY=<n> sets the
-// count, NOC_PERSIST_HEAVY_SPEC=0|2 the candidates (0 turns the default split off).
+// By default (cart-pole, N <= 320, #SIMDs < B <= 2 #SIMDs: the c3 slice of 2 GPUs) the costliest
+// #SIMDs / 8 trajectories of the probe order run two speculative candidates each beside the rest
+// on the two-wave instance: 2048 cart-poles 17.9 -> 16.3-16.8 ms (probe order alone;
+// profiles/r06/t/).  At one wave per SIMD (1024) the split made the light end of the order wait
+// for SIMDs: 11.4-11.6 ms on one batch but 16.2-18.5 ms on the c3 slices (profiles/r06/final_c4/),
+// so not there; at c3 (4096) it measured slower (profiles/r06/q/).  NOC_PERSIST_HEAVY=<n> sets
+// the count, NOC_PERSIST_HEAVY_SPEC=0|2 the candidates (0 turns the default split off).
 static int heavy_count(const noc_ipm_ws& w, int simds, bool* spec2) {
   const char* env = getenv("NOC_PERSIST_HEAVY");  // per launch (A/B sweeps in one process)
   const char* hs = getenv("NOC_PERSIST_HEAVY_SPEC");
@@ -856,8 +857,8 @@ static int heavy_count(const noc_ipm_ws& w, int simds, bool* spec2) {
     sp = hs && atoi(hs) == 2;
     if (w.Bt <= (sp ? simds / 2 : simds)) return 0;
   } else {
-    if ((hs && atoi(hs) == 0) || w.N > 320 || w.Bt <= simds / 2 || w.Bt > 2 * simds) return 0;
-    h = w.Bt <= simds ? simds / 4 : simds / 8;
+    if ((hs && atoi(hs) == 0) || w.N > 320 || w.Bt <= simds || w.Bt > 2 * simds) return 0;
+    h = simds / 8;
     sp = true;
   }
   if (h < 0) h = 0;

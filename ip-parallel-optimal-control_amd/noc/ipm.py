@@ -199,9 +199,8 @@ class BatchedIPM:
         tail = auto and not resume and self._tail_eligible()
         if auto:
             # the probe order also where the launcher splits off the costliest trajectories onto
-            # speculative candidates (cart-pole, #SIMDs / 2 < B <= 2 #SIMDs: ipm_persistent.hip
-            # heavy_count): 1024 cart-poles 13.3-14.0 -> 11.4-11.6 ms, 2048 20.4 -> 16.3-16.8 ms
-            # (profiles/r06/t/)
+            # speculative candidates (cart-pole, #SIMDs < B <= 2 #SIMDs: ipm_persistent.hip
+            # heavy_count): 2048 cart-poles 20.4 -> 16.3-16.8 ms (profiles/r06/t/)
             probe = not resume and (self.Bt > self._resident_slots() or self._heavy_split_eligible())
             schedule = "probe" if probe and not tail else "index"
         if schedule == "probe" and not resume:
@@ -222,8 +221,8 @@ class BatchedIPM:
             self._launch(mode, terminal, bp0, max_solves, resume=resume, order=self._order)
         return int(self.t["kkt_solves"].max().item()) if self.Bt else 0
 
-    # The tail schedule (opt-in, NOC_PERSIST_TAIL=1; superseded by the heavy split above) of a
-    # batch at one wave per SIMD (cart-pole, #SIMDs / 2 < B <= #SIMDs: the 4-GPU slice of c3):
+    # The tail of a batch at one wave per SIMD (cart-pole, #SIMDs / 2 < B <= #SIMDs: the 4-GPU
+    # slice of c3; NOC_PERSIST_TAIL=0 turns it off):
     # the launch is capped at solve counts TAIL_CAPS, and once the trajectories
     # still running fit two waves each on the SIMDs, they are gathered into a small workspace and
     # resumed there -- where the solver runs speculative candidates (two or four waves per
@@ -232,9 +231,8 @@ class BatchedIPM:
     # (capped-and-resumed solves and the candidates both are).  Measured (profiles/r06/o/): 1024
     # cart-poles 13.83-13.91 -> 13.30-13.34 ms with the caps below (cap 256: 205 still running,
     # resumed with four candidates); not at 2 waves per SIMD (2048: equal) nor after the probe
-    # launch (4096: 29-31 vs 25 ms -- it breaks the cost-ordered resume), so not there; the heavy
-    # split with candidates gets 1024 to 11.4-11.6 ms.  NOC_PERSIST_TAIL_CAPS="a,b,..." sets the
-    # caps.
+    # launch (4096: 29-31 vs 25 ms -- it breaks the cost-ordered resume), so not there.
+    # NOC_PERSIST_TAIL_CAPS="a,b,..." sets the caps.
     TAIL_CAPS = (256, 384, 512)
     _SHARED_FIELDS = ("x", "u", "x0") + tuple(_lib.WS_STATE_FIELDS) + tuple(_lib.WS_INT_FIELDS)
 
@@ -246,10 +244,10 @@ class BatchedIPM:
             return False
         simds = self._simds()
         return (self.persistent and self.family.kind == _lib.FAMILY_CARTPOLE and self.N <= 320
-                and simds < 2 * self.Bt <= 4 * simds)
+                and simds < self.Bt <= 2 * simds)
 
     def _tail_eligible(self) -> bool:
-        if os.environ.get("NOC_PERSIST_TAIL", "0") != "1" or os.environ.get("NOC_PERSIST_SPEC") == "1":
+        if os.environ.get("NOC_PERSIST_TAIL", "1") == "0" or os.environ.get("NOC_PERSIST_SPEC") == "1":
             return False
         if os.environ.get("NOC_PERSIST_STRUCT") == "0":
             return False

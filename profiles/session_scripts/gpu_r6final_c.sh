@@ -13,4 +13,3 @@ run 300 bench_c2.log python bench.py --problem pendulum --horizon 100 --batch 10
 run 300 bench_torchrun1.log python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --steps 10 --warmup 2 --no-cpu
 run 300 slices.log python tools/slice_curve.py --out $O/slices.json
 run 400 runtime_cartpole.log python tools/runtime_sweep.py --problem cartpole --out $O/runtime
-run 300 heavy_spec_1024.log python tools/heavy_spec.py --B 1024 --H 256
